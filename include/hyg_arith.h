@@ -1,0 +1,338 @@
+/*
+ * hyg_arith.h -- the deterministic arithmetic contract of hygeia_amd.
+ *
+ * Everything on the change-point inference path that decides an index (which
+ * ancestors survive resampling, which particle a backward trajectory picks)
+ * is computed with the primitives in this header, on the CPU oracle and in the
+ * HIP kernels alike, so that both produce bit-identical trajectories:
+ *
+ *   - hyg_exp / hyg_log: exp and log built from IEEE-754 basic operations only
+ *     (+ - * / floor, no FMA: every translation unit is compiled with
+ *     -ffp-contract=off). libm / ocml differ in the last ulp between host and
+ *     device; these do not. Accuracy is ~1 ulp (tests/test_arith.py pins them
+ *     against libm).
+ *   - exact fixed-point mass sums. The reference sums exp(weights) with
+ *     order-dependent float cumsums (resampling_functions.py:10,59; the TF
+ *     multinomial CDF behind tfd.Categorical.sample,
+ *     filter_and_smoother_algorithm.py:385,426). Here every such sum is an
+ *     exact integer sum, so it does not depend on summation order and any
+ *     parallel reduction tree on the GPU gives the oracle's value:
+ *       * resampling masses exp(f32 log-weight) are f32 values >= 2^-149 and
+ *         are summed EXACTLY in 192-bit integers scaled by 2^149 (no rounding
+ *         at all, the ideal the reference's f32 cumsum approximates);
+ *       * categorical masses exp(logit - max) (f64) are truncated to 2^-100
+ *         and summed exactly in 128-bit integers.
+ *   - Philox4x64-10 (Salmon et al., SC'11) counter-based uniforms keyed by
+ *     (seed, chain), countered by (stream, step, index): the "injected
+ *     randomness" both implementations consume. Pinned against numpy's Philox
+ *     in tests/test_arith.py.
+ *   - the packed 64-bit particle state (merged, d_ctrl, r_ctrl, d_case, r_case).
+ *
+ * C99-compatible so that the plain-C oracle (oracle/tg_oracle.c) includes it;
+ * under hipcc every function is __host__ __device__.
+ */
+#ifndef HYG_ARITH_H
+#define HYG_ARITH_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define HYG_HD __host__ __device__ __forceinline__
+#define HYG_FLOOR(x) __builtin_floor(x)
+#else
+#include <math.h>
+#define HYG_HD static inline
+#define HYG_FLOOR(x) floor(x)
+#endif
+
+/* ------------------------------------------------------------------ bits */
+HYG_HD uint64_t hyg_f64_bits(double x) { union { double d; uint64_t u; } c; c.d = x; return c.u; }
+HYG_HD double hyg_bits_f64(uint64_t u) { union { double d; uint64_t u; } c; c.u = u; return c.d; }
+HYG_HD uint32_t hyg_f32_bits(float x) { union { float f; uint32_t u; } c; c.f = x; return c.u; }
+HYG_HD float hyg_bits_f32(uint32_t u) { union { float f; uint32_t u; } c; c.u = u; return c.f; }
+
+#define HYG_INF (hyg_bits_f64(0x7ff0000000000000ull))
+#define HYG_NINF (hyg_bits_f64(0xfff0000000000000ull))
+#define HYG_NAN (hyg_bits_f64(0x7ff8000000000000ull))
+#define HYG_NINFF (hyg_bits_f32(0xff800000u))
+
+HYG_HD int hyg_isfinite(double x) { return (hyg_f64_bits(x) & 0x7ff0000000000000ull) != 0x7ff0000000000000ull; }
+HYG_HD int hyg_isfinitef(float x) { return (hyg_f32_bits(x) & 0x7f800000u) != 0x7f800000u; }
+
+/* 2^e as a double, e in [-1022, 1023] (exact). */
+HYG_HD double hyg_pow2(int e) { return hyg_bits_f64((uint64_t)(e + 1023) << 52); }
+
+/* ------------------------------------------------------------- exp / log */
+/* ln2 split: hi has 21 trailing zero bits so k*hi is exact for |k| < 2^11. */
+#define HYG_LN2_HI 6.93147180369123816490e-01
+#define HYG_LN2_LO 1.90821492927058770002e-10
+#define HYG_INV_LN2 1.44269504088896338700e+00
+
+/* exp(x) for double x. Range reduction x = k ln2 + r, |r| <= ln2/2, then the
+ * degree-13 Taylor polynomial of e^r by Horner (remainder < 4e-18), then an
+ * exact (or single-rounding, for subnormal results) scale by 2^k. */
+HYG_HD double hyg_exp(double x) {
+  if (x != x) return x;
+  if (x > 709.782712893383973096) return HYG_INF;
+  if (x < -745.13321910194110842) return 0.0;
+  const double kd = HYG_FLOOR(x * HYG_INV_LN2 + 0.5);
+  const int k = (int)kd;
+  const double hi = x - kd * HYG_LN2_HI;
+  const double lo = kd * HYG_LN2_LO;
+  const double r = hi - lo;
+  double p = 1.6059043836821614599e-10;  /* 1/13! */
+  p = 2.0876756987868098979e-09 + r * p; /* 1/12! */
+  p = 2.5052108385441718775e-08 + r * p; /* 1/11! */
+  p = 2.7557319223985890653e-07 + r * p; /* 1/10! */
+  p = 2.7557319223985890653e-06 + r * p; /* 1/9! */
+  p = 2.4801587301587301566e-05 + r * p; /* 1/8! */
+  p = 1.9841269841269841253e-04 + r * p; /* 1/7! */
+  p = 1.3888888888888888889e-03 + r * p; /* 1/6! */
+  p = 8.3333333333333332177e-03 + r * p; /* 1/5! */
+  p = 4.1666666666666664354e-02 + r * p; /* 1/4! */
+  p = 1.6666666666666665741e-01 + r * p; /* 1/3! */
+  p = 0.5 + r * p;
+  p = 1.0 + r * p;
+  p = 1.0 + r * p;
+  if (k > 1023) return (p * 2.0) * hyg_pow2(k - 1);
+  if (k >= -1021) return p * hyg_pow2(k);
+  /* subnormal result: exact scale into the normal range, then one rounding */
+  return (p * hyg_pow2(k + 54)) * hyg_pow2(-54);
+}
+
+/* log(x) for double x: x = 2^e m, m in (sqrt(1/2), sqrt(2)], f = m - 1,
+ * s = f/(2+f), log(1+f) = f - (f^2/2 - s (f^2/2 + R(s^2))) with the atanh
+ * series R(z) = sum_{i>=1} 2 z^i/(2i+1) to i = 11 (|s| <= 0.1716). */
+HYG_HD double hyg_log(double x) {
+  if (x != x || x < 0.0) return HYG_NAN;
+  if (x == 0.0) return HYG_NINF;
+  uint64_t b = hyg_f64_bits(x);
+  if ((b >> 52) == 0x7ff) return x; /* +inf */
+  int e = 0;
+  if ((b >> 52) == 0) { /* subnormal */
+    x = x * 18014398509481984.0; /* 2^54 */
+    b = hyg_f64_bits(x);
+    e = -54;
+  }
+  e += (int)((b >> 52) & 0x7ff) - 1023;
+  double m = hyg_bits_f64((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+  if (m > 1.41421356237309504880) { m = m * 0.5; e += 1; }
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  double R = 0.08695652173913043478; /* 2/23 */
+  R = 0.09523809523809523810 + z * R; /* 2/21 */
+  R = 0.10526315789473684211 + z * R; /* 2/19 */
+  R = 0.11764705882352941176 + z * R; /* 2/17 */
+  R = 0.13333333333333333333 + z * R; /* 2/15 */
+  R = 0.15384615384615384615 + z * R; /* 2/13 */
+  R = 0.18181818181818181818 + z * R; /* 2/11 */
+  R = 0.22222222222222222222 + z * R; /* 2/9 */
+  R = 0.28571428571428571429 + z * R; /* 2/7 */
+  R = 0.40000000000000000000 + z * R; /* 2/5 */
+  R = 0.66666666666666666667 + z * R; /* 2/3 */
+  R = z * R;
+  const double hfsq = 0.5 * f * f;
+  const double l1p = f - (hfsq - s * (hfsq + R));
+  const double ed = (double)e;
+  return ed * HYG_LN2_HI + (ed * HYG_LN2_LO + l1p);
+}
+
+/* f32 versions used where the reference computes in float32
+ * (resampling_functions.py:7-68): evaluated in double, rounded once. */
+HYG_HD float hyg_expf(float x) { return (float)hyg_exp((double)x); }
+HYG_HD float hyg_logf(float x) { return (float)hyg_log((double)x); }
+
+/* ------------------------------------------------------ 64-bit integer help */
+HYG_HD uint64_t hyg_mulhi64(uint64_t a, uint64_t b) {
+  const uint64_t a0 = a & 0xffffffffu, a1 = a >> 32, b0 = b & 0xffffffffu, b1 = b >> 32;
+  const uint64_t p00 = a0 * b0, p01 = a0 * b1, p10 = a1 * b0, p11 = a1 * b1;
+  const uint64_t mid = (p00 >> 32) + (p01 & 0xffffffffu) + (p10 & 0xffffffffu);
+  return p11 + (p01 >> 32) + (p10 >> 32) + (mid >> 32);
+}
+
+HYG_HD int hyg_clz64(uint64_t x) { return x ? __builtin_clzll(x) : 64; }
+
+/* ------------------------------------------------------------ u128 (F=100) */
+typedef struct { uint64_t lo, hi; } hyg_u128;
+
+HYG_HD hyg_u128 hyg_u128_zero(void) { hyg_u128 r; r.lo = 0; r.hi = 0; return r; }
+HYG_HD hyg_u128 hyg_u128_add(hyg_u128 a, hyg_u128 b) {
+  hyg_u128 r; r.lo = a.lo + b.lo; r.hi = a.hi + b.hi + (r.lo < a.lo ? 1u : 0u); return r;
+}
+HYG_HD int hyg_u128_lt(hyg_u128 a, hyg_u128 b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
+HYG_HD int hyg_u128_is_zero(hyg_u128 a) { return (a.lo | a.hi) == 0; }
+
+/* floor(e * 2^100) for e in [0, 1]; masses below 2^-100 become 0. */
+HYG_HD hyg_u128 hyg_fix100(double e) {
+  hyg_u128 r = hyg_u128_zero();
+  if (!(e > 0.0)) return r;
+  const uint64_t b = hyg_f64_bits(e);
+  const int E = (int)((b >> 52) & 0x7ff);
+  if (E == 0) return r;
+  const uint64_t mant = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
+  const int sh = E - 975; /* value*2^100 = mant * 2^(E-1075+100) */
+  if (sh >= 64) { r.hi = mant << (sh - 64); }
+  else if (sh > 0) { r.lo = mant << sh; r.hi = mant >> (64 - sh); }
+  else if (sh == 0) { r.lo = mant; }
+  else if (sh > -64) { r.lo = mant >> (-sh); }
+  return r;
+}
+
+/* value * 2^-scale as a double: the top 53 bits (truncated), exact scaling. */
+HYG_HD double hyg_u128_to_f64(hyg_u128 a, int scale) {
+  int p; uint64_t top;
+  if (a.hi) {
+    p = 127 - hyg_clz64(a.hi);
+  } else if (a.lo) {
+    p = 63 - hyg_clz64(a.lo);
+  } else {
+    return 0.0;
+  }
+  if (p <= 52) return (double)a.lo * hyg_pow2(-scale);
+  const int sh = p - 52; /* 1..75 */
+  if (sh >= 64) top = a.hi >> (sh - 64);
+  else top = (a.lo >> sh) | (a.hi << (64 - sh));
+  top &= 0x001fffffffffffffull;
+  return (double)top * hyg_pow2(sh - scale);
+}
+
+/* ------------------------------------------------------------ u192 (F=149) */
+typedef struct { uint64_t w0, w1, w2; } hyg_u192;
+
+HYG_HD hyg_u192 hyg_u192_zero(void) { hyg_u192 r; r.w0 = 0; r.w1 = 0; r.w2 = 0; return r; }
+HYG_HD hyg_u192 hyg_u192_add(hyg_u192 a, hyg_u192 b) {
+  hyg_u192 r;
+  r.w0 = a.w0 + b.w0;
+  const uint64_t c0 = r.w0 < a.w0 ? 1u : 0u;
+  const uint64_t t1 = a.w1 + b.w1;
+  const uint64_t c1a = t1 < a.w1 ? 1u : 0u;
+  r.w1 = t1 + c0;
+  const uint64_t c1b = r.w1 < t1 ? 1u : 0u;
+  r.w2 = a.w2 + b.w2 + c1a + c1b;
+  return r;
+}
+HYG_HD hyg_u192 hyg_u192_sub(hyg_u192 a, hyg_u192 b) { /* a >= b */
+  hyg_u192 r;
+  r.w0 = a.w0 - b.w0;
+  const uint64_t br0 = a.w0 < b.w0 ? 1u : 0u;
+  const uint64_t t1 = a.w1 - b.w1;
+  const uint64_t br1a = a.w1 < b.w1 ? 1u : 0u;
+  r.w1 = t1 - br0;
+  const uint64_t br1b = t1 < br0 ? 1u : 0u;
+  r.w2 = a.w2 - b.w2 - br1a - br1b;
+  return r;
+}
+HYG_HD int hyg_u192_is_zero(hyg_u192 a) { return (a.w0 | a.w1 | a.w2) == 0; }
+
+/* exact integer image of an f32 mass m in [0, 1]: m * 2^149. */
+HYG_HD hyg_u192 hyg_fix149f(float m) {
+  hyg_u192 r = hyg_u192_zero();
+  const uint32_t b = hyg_f32_bits(m);
+  if (b == 0 || (b >> 31)) return r;
+  const int E = (int)((b >> 23) & 0xff);
+  const uint64_t man = b & 0x7fffffu;
+  if (E == 0) { r.w0 = man; return r; }
+  const uint64_t v = man | 0x800000u;
+  const int sh = E - 1; /* 0..126 for m <= 1 */
+  if (sh < 64) {
+    r.w0 = v << sh;
+    r.w1 = sh ? (v >> (64 - sh)) : 0;
+  } else if (sh < 128) {
+    const int s2 = sh - 64;
+    r.w1 = v << s2;
+    r.w2 = s2 ? (v >> (64 - s2)) : 0;
+  } else {
+    r.w2 = v << (sh - 128);
+  }
+  return r;
+}
+
+/* value * 2^-149 as a double: top 53 bits (truncated), exactly scaled. */
+HYG_HD double hyg_u192_to_f64(hyg_u192 a) {
+  int p;
+  if (a.w2) p = 191 - hyg_clz64(a.w2);
+  else if (a.w1) p = 127 - hyg_clz64(a.w1);
+  else if (a.w0) p = 63 - hyg_clz64(a.w0);
+  else return 0.0;
+  uint64_t top;
+  int sh = p - 52;
+  if (sh <= 0) {
+    top = a.w0; /* p <= 52: value fits in w0 */
+    sh = 0;
+  } else if (sh < 64) {
+    top = (a.w0 >> sh) | (a.w1 << (64 - sh));
+  } else if (sh == 64) {
+    top = a.w1;
+  } else if (sh < 128) {
+    top = (a.w1 >> (sh - 64)) | (a.w2 << (128 - sh));
+  } else if (sh == 128) {
+    top = a.w2;
+  } else {
+    top = a.w2 >> (sh - 128);
+  }
+  top &= 0x001fffffffffffffull;
+  return (double)top * hyg_pow2(sh - 149);
+}
+
+/* ------------------------------------------------------- Philox4x64-10 */
+typedef struct { uint64_t v[4]; } hyg_ph4;
+
+HYG_HD hyg_ph4 hyg_philox4x64(uint64_t c0, uint64_t c1, uint64_t c2, uint64_t c3,
+                              uint64_t k0, uint64_t k1) {
+  hyg_ph4 x;
+  x.v[0] = c0; x.v[1] = c1; x.v[2] = c2; x.v[3] = c3;
+  for (int round = 0; round < 10; ++round) {
+    const uint64_t M0 = 0xD2E7470EE14C6C93ull, M1 = 0xCA5A826395121157ull;
+    const uint64_t hi0 = hyg_mulhi64(M0, x.v[0]), lo0 = M0 * x.v[0];
+    const uint64_t hi1 = hyg_mulhi64(M1, x.v[2]), lo1 = M1 * x.v[2];
+    hyg_ph4 y;
+    y.v[0] = hi1 ^ x.v[1] ^ k0;
+    y.v[1] = lo1;
+    y.v[2] = hi0 ^ x.v[3] ^ k1;
+    y.v[3] = lo0;
+    x = y;
+    k0 += 0x9E3779B97F4A7C15ull;
+    k1 += 0xBB67AE8584CAA73Bull;
+  }
+  return x;
+}
+
+/* Random streams (counter word 0). */
+#define HYG_RNG_PHANTOM 1u     /* initial phantom regime (case_control_distributions.py:67-74) */
+#define HYG_RNG_SYSTEMATIC 2u  /* systematic residual U (resampling_functions.py:58) */
+#define HYG_RNG_MULTINOMIAL 3u /* unbiased-fallback categorical draws (resampling_functions.py:46) */
+#define HYG_RNG_BACKWARD 4u    /* backward-simulation categorical draws (filter_and_smoother_algorithm.py:385,426) */
+
+/* 64 random bits number `index` of (stream, step) for chain (seed, chain_id). */
+HYG_HD uint64_t hyg_rand64(uint64_t seed, uint64_t chain_id, uint32_t stream, uint64_t step, uint64_t index) {
+  const hyg_ph4 r = hyg_philox4x64((uint64_t)stream, step, index >> 2, 0, seed, chain_id);
+  return r.v[index & 3];
+}
+
+/* f32 uniform on [0, 1) from 24 random bits (exact). */
+HYG_HD float hyg_u01f(uint64_t r) { return (float)(r >> 40) * 5.9604644775390625e-08f; }
+
+/* floor(r * total / 2^64): an integer uniform on [0, total) for total < 2^114. */
+HYG_HD hyg_u128 hyg_scale_target(uint64_t r, hyg_u128 total) {
+  hyg_u128 t;
+  t.lo = r * total.hi;
+  t.hi = hyg_mulhi64(r, total.hi);
+  hyg_u128 add; add.lo = hyg_mulhi64(r, total.lo); add.hi = 0;
+  return hyg_u128_add(t, add);
+}
+
+/* ------------------------------------------------------ packed particle */
+/* bits [0,24) d_ctrl, [24,48) d_case, [48,54) r_ctrl, [54,60) r_case, [60] merged */
+#define HYG_DMAX 0xffffff
+HYG_HD uint64_t hyg_st_pack(int m, int dc, int rc, int dk, int rk) {
+  return (uint64_t)(uint32_t)dc | ((uint64_t)(uint32_t)dk << 24) | ((uint64_t)rc << 48) |
+         ((uint64_t)rk << 54) | ((uint64_t)m << 60);
+}
+HYG_HD int hyg_st_m(uint64_t s) { return (int)((s >> 60) & 1u); }
+HYG_HD int hyg_st_dc(uint64_t s) { return (int)(s & 0xffffffu); }
+HYG_HD int hyg_st_dk(uint64_t s) { return (int)((s >> 24) & 0xffffffu); }
+HYG_HD int hyg_st_rc(uint64_t s) { return (int)((s >> 48) & 63u); }
+HYG_HD int hyg_st_rk(uint64_t s) { return (int)((s >> 54) & 63u); }
+
+#endif /* HYG_ARITH_H */

@@ -1,0 +1,259 @@
+/*
+ * hyg_model.h -- host-side construction of the two-group model's constants
+ * and lookup tables (C99, libm). Shared by the product's host library
+ * (hygeia_amd/csrc/tg_host.cpp) and by the CPU oracle (oracle/tg_oracle.c):
+ * the tables are inputs of the inference, so both sides must consume the same
+ * values; tests/test_model_tables.py pins them against scipy independently.
+ *
+ * What is tabulated (so that no transcendental is evaluated per particle):
+ *  - Beta-Binomial log-gamma tables: BB(y | n, a, b) = lC(n, y) + lgamma(y + a)
+ *    + lgamma(n - y + b) - lgamma(n + a + b) + lgamma(a + b) - lgamma(a) - lgamma(b)
+ *    (tfd.BetaBinomial.log_prob at case_control_regime_model.py:221-226).
+ *  - the change-point hazard rho_g(d, r) of case_control_regime_model.py:111-168:
+ *    rho = 0 for d < u; otherwise h / S with h = NegBin_pmf(d - u; kappa, p_g[r])
+ *    and S = exp(log1p(-cdf(d - u - 1))) (S = 1 when d == u); rho -> 0.1 when
+ *    not finite. The reference evaluates the cdf in float32, so S underflows to
+ *    0 (rho = 0.1) once the cdf rounds to 1.0f; that rounding is reproduced
+ *    (the cdf is rounded to float before log1p), the rest is exact double.
+ */
+#ifndef HYG_MODEL_H
+#define HYG_MODEL_H
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "hygeia_amd.h"
+
+typedef struct hyg_tg_consts {
+  int32_t K, u, M, B, I, Nmax;
+  int32_t optimal, multinomial;
+  double alpha[HYG_KMAX], beta[HYG_KMAX];
+  double p_ctrl[HYG_KMAX], p_case[HYG_KMAX]; /* NegBin success probabilities */
+  double kappa_ctrl, kappa_case;
+  double lPc[HYG_KMAX * HYG_KMAX]; /* log P_ctrl[r][r'], diagonal -inf */
+  double lPm[4];                   /* log P(m' | m), [m*2 + m'] */
+  double lU1, lU2;                 /* log 1/(K-1), log 1/(K-2) (-inf if K == 2) */
+  double log_M;                    /* log(M) */
+  float sig_thresh;                /* log-weights below this never matter */
+  int32_t _pad;
+} hyg_tg_consts;
+
+static inline double hyg__lse(const double* v, int n) {
+  double mx = -INFINITY;
+  for (int i = 0; i < n; ++i) if (v[i] > mx) mx = v[i];
+  if (!isfinite(mx)) return mx;
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += exp(v[i] - mx);
+  return mx + log(s);
+}
+
+static inline double hyg__f32(double x) { return (double)(float)x; }
+
+/* Derives the model constants from the CLI-level parameters, mirroring
+ * run_inference_two_groups.py:110-167 and get_estimated_control_group_param
+ * (:76-89). The reference keeps every parameter in a float32 tf.Variable: the
+ * parameter VALUES are rounded to float32 here as well, the arithmetic on them
+ * is double. Returns HYG_OK or HYG_EINVAL. */
+static inline int hyg_tg_derive(const hyg_tg_params* pr, hyg_tg_consts* c) {
+  memset(c, 0, sizeof(*c));
+  const int32_t theta_len = pr->theta_len;
+  const int K = pr->n_regimes;
+  if (K < 2 || K > HYG_KMAX) return HYG_EINVAL;
+  if (pr->minimum_duration < 0 || pr->num_resampled_ancestors < 1 || pr->num_samples_backward < 1) return HYG_EINVAL;
+  if ((int64_t)pr->num_resampled_ancestors * (2 * K + K * K) > (1 << 22)) return HYG_EINVAL;
+  c->K = K;
+  c->u = pr->minimum_duration;
+  c->M = pr->num_resampled_ancestors;
+  c->B = pr->num_samples_backward;
+  c->I = 2 * K + K * K;
+  c->Nmax = c->M * c->I;
+  c->optimal = pr->optimal_resampling ? 1 : 0;
+  c->multinomial = pr->multinomial ? 1 : 0;
+  /* T4: Beta parameters by method of moments (case_control_regime_model.py:19-23) */
+  for (int r = 0; r < K; ++r) {
+    const double mu = hyg__f32(pr->mu[r]), sg = hyg__f32(pr->sigma[r]);
+    const double nu = mu * (1.0 - mu) / (sg * sg) - 1.0;
+    c->alpha[r] = mu * nu;
+    c->beta[r] = (1.0 - mu) * nu;
+    if (!(c->alpha[r] > 0.0) || !(c->beta[r] > 0.0) || !isfinite(c->alpha[r]) || !isfinite(c->beta[r]))
+      return HYG_EINVAL;
+  }
+  /* T1: control transition matrix and omega from theta (:76-89). theta holds
+   * K(K-1) off-diagonal log-weights row by row; omega_logit = LAST K entries. */
+  const int need = K * (K - 1) + K;
+  if (theta_len < need || theta_len > HYG_KMAX * HYG_KMAX) return HYG_EINVAL;
+  int i = 0;
+  for (int r = 0; r < K; ++r) {
+    double e[HYG_KMAX], s = 0.0;
+    for (int r1 = 0; r1 < K; ++r1) {
+      e[r1] = 0.0;
+      if (r1 != r) { e[r1] = exp(pr->theta[i++]); s += e[r1]; }
+    }
+    double v[HYG_KMAX];
+    int n = 0;
+    for (int r1 = 0; r1 < K; ++r1)
+      if (r1 != r) v[n++] = hyg__f32(log(e[r1] / s)); /* P_softmax_control Variable (f32) */
+    /* regime_probs = softmax(set_diag(P, -inf)) (case_control_regime_model.py:90-94) */
+    const double lse = hyg__lse(v, n);
+    n = 0;
+    for (int r1 = 0; r1 < K; ++r1)
+      c->lPc[r * K + r1] = (r1 == r) ? -INFINITY : v[n++] - lse;
+  }
+  for (int r = 0; r < K; ++r) {
+    const double th = hyg__f32(pr->theta[theta_len - K + r]);
+    c->p_ctrl[r] = hyg__f32(1.0 / (1.0 + exp(-th))); /* omega_control (:145-149) */
+    c->p_case[r] = hyg__f32(pr->omega_case);          /* omega_case (:144)        */
+    if (!(c->p_ctrl[r] > 0.0 && c->p_ctrl[r] < 1.0) || !(c->p_case[r] > 0.0 && c->p_case[r] < 1.0))
+      return HYG_EINVAL;
+  }
+  c->kappa_ctrl = hyg__f32(pr->kappa_control);
+  c->kappa_case = hyg__f32(pr->kappa_case);
+  if (!(c->kappa_ctrl > 0.0) || !(c->kappa_case > 0.0)) return HYG_EINVAL;
+  /* T2: merged-state transition (:164-167), rows m = 0 (split), 1 (merged) */
+  {
+    const double qs = pr->split_prob, mlp = pr->merge_log_prob;
+    if (!(qs > 0.0 && qs < 1.0) || !(mlp < 0.0)) return HYG_EINVAL;
+    double v0[2] = {hyg__f32(log(1.0 - exp(mlp))), hyg__f32(mlp)};
+    double v1[2] = {hyg__f32(log(qs)), hyg__f32(log(1.0 - qs))};
+    const double l0 = hyg__lse(v0, 2), l1 = hyg__lse(v1, 2);
+    c->lPm[0] = v0[0] - l0;
+    c->lPm[1] = v0[1] - l0;
+    c->lPm[2] = v1[0] - l1;
+    c->lPm[3] = v1[1] - l1;
+  }
+  c->lU1 = -log((double)(K - 1));
+  c->lU2 = (K > 2) ? -log((double)(K - 2)) : -INFINITY;
+  c->log_M = log((double)c->M);
+  c->sig_thresh = (float)(-(110.0 + c->log_M));
+  return HYG_OK;
+}
+
+/* ------------------------------------------------------- NegBin / betainc */
+static inline double hyg_lbeta(double a, double b) { return lgamma(a) + lgamma(b) - lgamma(a + b); }
+
+/* continued fraction of the regularized incomplete beta (modified Lentz) */
+static inline double hyg__betacf(double a, double b, double x) {
+  const double tiny = 1e-300;
+  double qab = a + b, qap = a + 1.0, qam = a - 1.0;
+  double cc = 1.0, d = 1.0 - qab * x / qap;
+  if (fabs(d) < tiny) d = tiny;
+  d = 1.0 / d;
+  double h = d;
+  for (int m = 1; m <= 100000; ++m) {
+    const double m2 = 2.0 * m;
+    double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+    d = 1.0 + aa * d; if (fabs(d) < tiny) d = tiny;
+    cc = 1.0 + aa / cc; if (fabs(cc) < tiny) cc = tiny;
+    d = 1.0 / d; h *= d * cc;
+    aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+    d = 1.0 + aa * d; if (fabs(d) < tiny) d = tiny;
+    cc = 1.0 + aa / cc; if (fabs(cc) < tiny) cc = tiny;
+    d = 1.0 / d;
+    const double del = d * cc;
+    h *= del;
+    if (fabs(del - 1.0) < 1e-16) break;
+  }
+  return h;
+}
+
+/* I_x(a, b), the regularized incomplete beta function */
+static inline double hyg_betainc(double a, double b, double x) {
+  if (x <= 0.0) return 0.0;
+  if (x >= 1.0) return 1.0;
+  const double lbt = a * log(x) + b * log1p(-x) - hyg_lbeta(a, b);
+  if (x < (a + 1.0) / (a + b + 2.0)) return exp(lbt) * hyg__betacf(a, b, x) / a;
+  return 1.0 - exp(lbt) * hyg__betacf(b, a, 1.0 - x) / b;
+}
+
+/* tfd.NegativeBinomial(total_count=kappa, probs=p): pmf(x) = C(x+kappa-1, x) (1-p)^kappa p^x */
+static inline double hyg_nb_logpmf(double x, double kappa, double p) {
+  return lgamma(x + kappa) - lgamma(kappa) - lgamma(x + 1.0) + kappa * log1p(-p) + x * log(p);
+}
+/* P(X > x) = I_p(x + 1, kappa) */
+static inline double hyg_nb_sf(double x, double kappa, double p) {
+  if (x < 0.0) return 1.0;
+  return hyg_betainc(x + 1.0, kappa, p);
+}
+
+/* rho(d) as the reference computes it (see header comment). */
+static inline double hyg_hazard_rho(int d, int u, double kappa, double p) {
+  if (d < u) return 0.0;
+  const double x = (double)(d - u);
+  const double log_h = hyg_nb_logpmf(x, kappa, p);
+  double log_s = 0.0;
+  if (d > u) {
+    const float cdf_f = (float)(1.0 - hyg_nb_sf(x - 1.0, kappa, p));
+    log_s = log1p(-(double)cdf_f);
+  }
+  if (log_h == -INFINITY) return 0.0;
+  const double rho = exp(log_h - log_s);
+  return isfinite(rho) ? rho : 0.1;
+}
+
+/* smallest d > u at which the float32 cdf has saturated (rho == 0.1 from
+ * there on), or dmax + 1 if it does not saturate up to dmax */
+static inline int hyg_hazard_dsat(int u, double kappa, double p, int dmax) {
+  /* the cdf is monotone: bisection on "cdf(d - u - 1) rounds to 1.0f" */
+  int lo = u + 1, hi = dmax + 1;
+  if (lo > dmax) return dmax + 1;
+  while (lo < hi) {
+    const int mid = lo + (hi - lo) / 2;
+    const float cdf_f = (float)(1.0 - hyg_nb_sf((double)(mid - u - 1), kappa, p));
+    if (cdf_f == 1.0f) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+/* Table length Dcap covering durations [0, Dcap); lookups clamp d >= Dcap to
+ * Dcap - 1, which is exact because every row is constant from its
+ * saturation point on (and Dcap > max_duration otherwise). */
+static inline int hyg_hazard_len(const hyg_tg_consts* c, int max_duration) {
+  int dcap = c->u + 2;
+  for (int g = 0; g < 2; ++g)
+    for (int r = 0; r < c->K; ++r) {
+      const double kap = g ? c->kappa_case : c->kappa_ctrl;
+      const double p = g ? c->p_case[r] : c->p_ctrl[r];
+      const int ds = hyg_hazard_dsat(c->u, kap, p, max_duration);
+      if (ds + 1 > dcap) dcap = ds + 1;
+    }
+  return dcap;
+}
+
+/* hz[((g*K + r)*Dcap + d)*2 + 0] = log rho, [...+1] = log(1 - rho) */
+static inline void hyg_hazard_fill(const hyg_tg_consts* c, int dcap, double* hz) {
+  for (int g = 0; g < 2; ++g)
+    for (int r = 0; r < c->K; ++r) {
+      const double kap = g ? c->kappa_case : c->kappa_ctrl;
+      const double p = g ? c->p_case[r] : c->p_ctrl[r];
+      const int ds = hyg_hazard_dsat(c->u, kap, p, dcap - 1);
+      double* row = hz + (size_t)(g * c->K + r) * dcap * 2;
+      for (int d = 0; d < dcap; ++d) {
+        const double rho = (d >= ds) ? 0.1 : hyg_hazard_rho(d, c->u, kap, p);
+        row[2 * d + 0] = log(rho);
+        row[2 * d + 1] = (rho >= 1.0) ? -INFINITY : log1p(-rho);
+      }
+    }
+}
+
+/* Beta-Binomial tables for counts 0..nmax:
+ *   lf[j] = lgamma(j + 1)
+ *   lg[(r*3 + 0)*(nmax+1) + j] = lgamma(j + alpha_r)
+ *   lg[(r*3 + 1)*(nmax+1) + j] = lgamma(j + beta_r)
+ *   lg[(r*3 + 2)*(nmax+1) + j] = lgamma(j + alpha_r + beta_r)
+ *   cst[r] = lgamma(alpha_r + beta_r) - lgamma(alpha_r) - lgamma(beta_r) */
+static inline void hyg_bb_tables(const hyg_tg_consts* c, int nmax, double* lf, double* lg, double* cst) {
+  const int L = nmax + 1;
+  for (int j = 0; j < L; ++j) lf[j] = lgamma((double)j + 1.0);
+  for (int r = 0; r < c->K; ++r) {
+    const double a = c->alpha[r], b = c->beta[r];
+    for (int j = 0; j < L; ++j) {
+      lg[(size_t)(r * 3 + 0) * L + j] = lgamma((double)j + a);
+      lg[(size_t)(r * 3 + 1) * L + j] = lgamma((double)j + b);
+      lg[(size_t)(r * 3 + 2) * L + j] = lgamma((double)j + a + b);
+    }
+    cst[r] = lgamma(a + b) - lgamma(a) - lgamma(b);
+  }
+}
+
+#endif /* HYG_MODEL_H */

@@ -1,0 +1,157 @@
+/*
+ * hygeia_amd.h -- C ABI of the MI355X-native Hygeia change-point inference path.
+ *
+ * Drop-in boundary for the two-group (case/control) inference engine of
+ * ucl-medical-genomics/hygeia. The reference exposes this path as
+ *
+ *   filter_and_smoother_algorithm.run(observations, initial_state_prior,
+ *       initial_proposal, transition_fn, observation_fn, num_particles,
+ *       proposal_fn, num_resampled_ancestors, optimal_resampling,
+ *       multinomial_resampling, num_simulations)
+ *     -> (BackwardSimulationResults(particle={merged_state [T,B],
+ *          control_state [T,B,2], case_state [T,B,2]}),
+ *         final_unnormalized_log_weights [N_max])
+ *   (src/two_group/hygeia/filter_and_smoother_algorithm.py:38-138)
+ *
+ * with the model (CaseControlRegimeModel, case_control_regime_model.py:41-244)
+ * and the proposal (CaseControlProposal, case_control_proposal_mappings.py:3-216)
+ * passed in as Python callables, driven by
+ * src/two_group/run_inference_two_groups.py:92-322 ("hygeia infer"). Here the
+ * model is fixed (it is the only one the CLI builds) and given by its
+ * parameters; everything else is plain pointers and sizes.
+ *
+ * Conventions: every entry point returns HYG_OK (0) or a negative HYG_E* code
+ * and never throws; hyg_last_error() gives a thread-local message. The caller
+ * owns every buffer. Functions taking a `stream` argument enqueue work on that
+ * hipStream_t (NULL = the default stream) and take DEVICE pointers; functions
+ * named *_host take host pointers and synchronise. There is no CPU fallback:
+ * without a HIP device every compute entry point returns HYG_EDEVICE.
+ */
+#ifndef HYGEIA_AMD_H
+#define HYGEIA_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HYG_KMAX 16
+
+#define HYG_OK 0
+#define HYG_EINVAL (-1)
+#define HYG_ENUMERIC (-2) /* all particle weights became -inf */
+#define HYG_EDEVICE (-3)
+#define HYG_ENOMEM (-4)
+#define HYG_EUNSUPPORTED (-5)
+
+/* Parameters of the two-group model as "hygeia infer" receives them
+ * (absl flags at run_inference_two_groups.py:19-72, theta file at :76-89,
+ * fixed kappa at :158-161). */
+typedef struct hyg_tg_params {
+  int32_t n_regimes;               /* K = len(--mu) (:126)                        */
+  int32_t minimum_duration;        /* u, --minimum_duration, default 3 (:25-27)   */
+  int32_t num_resampled_ancestors; /* M, --num_resampled_particles, default 50     */
+  int32_t num_samples_backward;    /* B, --num_samples_backward, default 25       */
+  int32_t optimal_resampling;      /* 1 on the CLI path (:274)                    */
+  int32_t multinomial;             /* --multinomial; used only when optimal == 0  */
+  int32_t theta_len;               /* number of values in theta (K^2 on the CLI)  */
+  int32_t _pad;
+  double mu[HYG_KMAX];             /* --mu (float32 in the reference)             */
+  double sigma[HYG_KMAX];          /* --sigma                                     */
+  double theta[HYG_KMAX * HYG_KMAX]; /* theta_{chrom}.csv.gz 'data': K(K-1) log-p
+                                        blocks, then K logit-omega (:76-89)       */
+  double omega_case;               /* --omega_case, default 0.8 (:28-30)          */
+  double merge_log_prob;           /* --merge_log_prob, default log(0.1) (:31-33) */
+  double split_prob;               /* --split_prob, default 0.01 (:34-36)         */
+  double kappa_control;            /* 2 (:158-159)                                */
+  double kappa_case;               /* 2 (:160-161)                                */
+} hyg_tg_params;
+
+/* Fills p with the reference's flag defaults (K = 6, uniform theta). */
+void hyg_tg_params_default(hyg_tg_params* p);
+
+/* One chain = one (chromosome, segment, seed) task of modules/two_group/4_infer.nf,
+ * i.e. one run_inference_two_groups.py process. */
+typedef struct hyg_tg_chain {
+  int64_t site_begin; /* first site of the chain in the site-major input arrays  */
+  int32_t n_sites;    /* T (segment + buffers, run_inference_two_groups.py:199-200) */
+  int32_t _pad;
+  uint64_t seed;      /* --seed                                                  */
+  uint64_t chain_id;  /* RNG stream id of the chain (e.g. chrom*2^32 + batch)    */
+  int64_t out_begin;  /* first output row of the chain in the output arrays      */
+} hyg_tg_chain;
+
+typedef struct hyg_tg_model hyg_tg_model; /* opaque: derived constants + tables */
+
+/* Builds the model: derived constants (T2/T4 of SURVEY 8a), Beta-Binomial
+ * log-gamma tables for read counts <= max_total_reads, and the hazard tables
+ * (case_control_regime_model.py:111-168) for durations <= max_duration.
+ * Uploads the tables to the current HIP device when one is present. */
+int hyg_tg_model_create(const hyg_tg_params* params, int32_t max_total_reads,
+                        int32_t max_duration, hyg_tg_model** out);
+void hyg_tg_model_destroy(hyg_tg_model* model);
+
+/* Derived sizes: I = 2K + K^2 proposal slots, N_max = M * I particles
+ * (run_inference_two_groups.py:263,285). */
+int32_t hyg_tg_num_particles(const hyg_tg_model* model);
+
+/* Per-site emission table E[t][g*K + r] = log g_t for group g (0 control,
+ * 1 case) and regime r: sum over samples of BetaBinomial(meth | total,
+ * alpha_r, beta_r) (case_control_regime_model.py:197-231). Counts are
+ * site-major uint16 [T][S]. Device pointers. */
+int hyg_tg_emission(const hyg_tg_model* model, const uint16_t* meth_ctrl, const uint16_t* tot_ctrl,
+                    int32_t s_ctrl, const uint16_t* meth_case, const uint16_t* tot_case, int32_t s_case,
+                    int64_t n_sites, double* emission, void* stream);
+
+/* Workspace bytes for the forward->backward ancestor history of `n_chains`
+ * chains totalling `total_steps` filter steps. */
+size_t hyg_tg_workspace_bytes(const hyg_tg_model* model, int32_t n_chains, int64_t total_steps);
+
+/* Outputs of hyg_tg_run_chains, all device pointers indexed by out_begin + t:
+ * trajectories as the reference saves them (run_inference_two_groups.py:299-314):
+ *   merged [T][B] int16, control [T][B][2] int16 (d, r), case [T][B][2] int16,
+ *   split_probs [T] f32, regime_probs [T][2K] f32 (test_function means, :233-240,294-296),
+ * per chain: log_z [n_chains] f64 (logsumexp of the final weights, :289-290) and
+ * optionally final_log_weights [n_chains][N_max] f64 (the second return value
+ * of run(), -inf padded; may be NULL), status [n_chains] int32 (HYG_OK or
+ * HYG_ENUMERIC per chain; may be NULL). */
+typedef struct hyg_tg_outputs {
+  int16_t* merged;
+  int16_t* control;
+  int16_t* kase;
+  float* split_probs;
+  float* regime_probs;
+  double* log_z;
+  double* final_log_weights;
+  int32_t* status;
+} hyg_tg_outputs;
+
+/* Runs the particle filter with optimal finite-state resampling followed by
+ * backward simulation (filter_and_smoother_algorithm.py:38-138, 141-288,
+ * 368-447) for `n_chains` independent chains, one workgroup per chain.
+ * `chains` is a HOST array; `emission` is the device table of
+ * hyg_tg_emission; `workspace` has hyg_tg_workspace_bytes bytes. */
+int hyg_tg_run_chains(const hyg_tg_model* model, const hyg_tg_chain* chains, int32_t n_chains,
+                      const double* emission, void* workspace, size_t workspace_bytes,
+                      const hyg_tg_outputs* outputs, void* stream);
+
+/* Host-pointer convenience: one chain of T sites (the whole of one
+ * run_inference_two_groups.py invocation). Outputs are host arrays sized as
+ * above for one chain; final_log_weights may be NULL. */
+int hyg_tg_run_chain_host(const hyg_tg_model* model, const uint16_t* meth_ctrl, const uint16_t* tot_ctrl,
+                          int32_t s_ctrl, const uint16_t* meth_case, const uint16_t* tot_case, int32_t s_case,
+                          int32_t n_sites, uint64_t seed, uint64_t chain_id, int16_t* merged, int16_t* control,
+                          int16_t* kase, float* split_probs, float* regime_probs, double* log_z,
+                          double* final_log_weights);
+
+/* Number of visible HIP devices (0 when none: compute calls then fail). */
+int hyg_device_count(void);
+const char* hyg_last_error(void);
+const char* hyg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYGEIA_AMD_H */

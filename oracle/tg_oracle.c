@@ -1,0 +1,537 @@
+/*
+ * tg_oracle.c -- CPU ORACLE for the two-group change-point inference path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is a sequential, plain-C restatement of the
+ * reference algorithm, used by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py as the CHECKER. It is never linked into, called
+ * by or shipped with the product (hygeia_amd/), which runs on the GPU only.
+ *
+ * It restates, step for step (reference = /root/reference/src/two_group):
+ *   - the emission, observation_fn        hygeia/case_control_regime_model.py:197-231
+ *   - the transition, transition_fn        hygeia/case_control_regime_model.py:80-193
+ *                                          hygeia/case_control_distributions.py:138-151, 246-291
+ *   - the initial (phantom) prior          case_control_regime_model.py:234-244,
+ *                                          case_control_distributions.py:59-74
+ *   - the deterministic proposal _xi       hygeia/case_control_proposal_mappings.py:11-103, 106-134, 175-216
+ *   - the filter steps                     hygeia/filter_and_smoother_algorithm.py:141-172 (t = 0), 176-288
+ *   - optimal finite-state resampling      hygeia/resampling_functions.py:7-52, systematic :56-69
+ *   - unbiased resampling                  hygeia/resampling_functions.py:71-79
+ *   - backward simulation                  hygeia/filter_and_smoother_algorithm.py:368-447,
+ *                                          hygeia/smoothing_functions.py:46-59
+ *   - the posterior functionals            run_inference_two_groups.py:233-240, 289-296
+ * with the arithmetic contract of include/hyg_arith.h (exact mass sums,
+ * deterministic exp/log, Philox streams) and the tables of include/hyg_model.h.
+ *
+ * Parity status: the reference (TensorFlow 2.3 / TFP 0.11) is not importable
+ * in this container, so whole-chain outputs are "parity unpinned" against the
+ * reference itself; sub-functions are pinned against scipy and the known
+ * answers of SURVEY.md Appendix C (tests/test_model_tables.py,
+ * tests/test_oracle.py), and the chain is cross-checked against an independent
+ * numpy restatement (oracle/tg_oracle_np.py).
+ *
+ * Build: make -C oracle  (gcc -O2 -ffp-contract=off -fPIC -shared)
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/hyg_arith.h"
+#include "../include/hyg_model.h"
+
+typedef struct {
+  hyg_tg_consts c;
+  int dcap;
+  double* hz; /* [2][K][dcap][2] */
+} oracle_model;
+
+static int om_init(oracle_model* om, const hyg_tg_params* p, int max_duration) {
+  int rc = hyg_tg_derive(p, &om->c);
+  if (rc) return rc;
+  om->dcap = hyg_hazard_len(&om->c, max_duration);
+  om->hz = (double*)malloc(sizeof(double) * 2 * 2 * om->c.K * (size_t)om->dcap);
+  if (!om->hz) return HYG_ENOMEM;
+  hyg_hazard_fill(&om->c, om->dcap, om->hz);
+  return HYG_OK;
+}
+static void om_free(oracle_model* om) { free(om->hz); }
+
+static inline const double* om_hz(const oracle_model* om, int g, int r, int d) {
+  if (d >= om->dcap) d = om->dcap - 1;
+  if (d < 0) d = 0;
+  return om->hz + ((size_t)(g * om->c.K + r) * om->dcap + d) * 2;
+}
+
+/* ------------------------------------------------------------ emission */
+/* observation_fn: sum over samples of BetaBinomial(meth | total, alpha_r, beta_r),
+ * control regimes then case regimes; n == 0 contributes exactly 0 (TFP). */
+int oracle_tg_emission(const hyg_tg_params* p, const uint16_t* meth_c, const uint16_t* tot_c, int s_c,
+                       const uint16_t* meth_k, const uint16_t* tot_k, int s_k, int64_t T, double* E) {
+  hyg_tg_consts c;
+  int rc = hyg_tg_derive(p, &c);
+  if (rc) return rc;
+  const int K = c.K;
+  int nmax = 0;
+  for (int64_t i = 0; i < T * s_c; ++i) {
+    if (meth_c[i] > tot_c[i]) return HYG_EINVAL;
+    if (tot_c[i] > nmax) nmax = tot_c[i];
+  }
+  for (int64_t i = 0; i < T * s_k; ++i) {
+    if (meth_k[i] > tot_k[i]) return HYG_EINVAL;
+    if (tot_k[i] > nmax) nmax = tot_k[i];
+  }
+  const int L = nmax + 1;
+  double* lf = (double*)malloc(sizeof(double) * L);
+  double* lg = (double*)malloc(sizeof(double) * (size_t)3 * K * L);
+  double cst[HYG_KMAX];
+  if (!lf || !lg) { free(lf); free(lg); return HYG_ENOMEM; }
+  hyg_bb_tables(&c, nmax, lf, lg, cst);
+  for (int64_t t = 0; t < T; ++t) {
+    for (int g = 0; g < 2; ++g) {
+      const int S = g ? s_k : s_c;
+      const uint16_t* my = g ? meth_k + t * s_k : meth_c + t * s_c;
+      const uint16_t* nt = g ? tot_k + t * s_k : tot_c + t * s_c;
+      for (int r = 0; r < K; ++r) {
+        const double* LA = lg + (size_t)(r * 3 + 0) * L;
+        const double* LB = lg + (size_t)(r * 3 + 1) * L;
+        const double* LAB = lg + (size_t)(r * 3 + 2) * L;
+        double e = 0.0;
+        for (int s = 0; s < S; ++s) {
+          const int n = nt[s], y = my[s];
+          if (n == 0) continue;
+          double term = lf[n] - lf[y];
+          term = term - lf[n - y];
+          term = term + LA[y];
+          term = term + LB[n - y];
+          term = term - LAB[n];
+          term = term + cst[r];
+          e = e + term;
+        }
+        E[t * 2 * K + g * K + r] = e;
+      }
+    }
+  }
+  free(lf);
+  free(lg);
+  return HYG_OK;
+}
+
+/* ---------------------------------------------------------- transition */
+/* log f_t(next | prev) for t >= 1 (transition_fn(step, prev).log_prob(next)):
+ * log P(m'|m) + log f_ctrl + log f_case, summed in that order. */
+static double tg_trans(const oracle_model* om, uint64_t prev, uint64_t next) {
+  const hyg_tg_consts* c = &om->c;
+  const int K = c->K;
+  const int m = hyg_st_m(prev), dc = hyg_st_dc(prev), rc = hyg_st_rc(prev), dk = hyg_st_dk(prev),
+            rk = hyg_st_rk(prev);
+  const int m2 = hyg_st_m(next), dc2 = hyg_st_dc(next), rc2 = hyg_st_rc(next), dk2 = hyg_st_dk(next),
+            rk2 = hyg_st_rk(next);
+  /* _next_merged_state_probs (case_control_regime_model.py:80-87) */
+  double lm;
+  if ((dk < dc ? dk : dc) >= c->u) lm = c->lPm[m * 2 + m2];
+  else lm = (m2 == m) ? 0.0 : -INFINITY;
+  /* ControlStateTransition._log_prob (case_control_distributions.py:138-151) */
+  const double* hc = om_hz(om, 0, rc, dc);
+  double lc;
+  if (dc2 == 1) lc = hc[0] + c->lPc[rc * K + rc2];
+  else lc = (dc2 == dc + 1 && rc2 == rc) ? hc[1] : -INFINITY;
+  /* CaseStateTransition._log_prob (case_control_distributions.py:246-291) */
+  double lk;
+  if (m2 == 1) {
+    lk = (rk2 == rc2 && dk2 == dc2) ? 0.0 : -INFINITY;
+  } else if (m == 1 && dc2 != 1) {
+    lk = (dk2 == 1 && rk2 != rc2) ? c->lU1 : -INFINITY;
+  } else if (rc2 == rk && m == 0) {
+    lk = (dk2 == 1 && rk2 != rc2) ? c->lU1 : -INFINITY;
+  } else {
+    const double* hk = om_hz(om, 1, rk, dk);
+    if (dk2 == 1) lk = (rk2 != rc2 && rk2 != rk) ? hk[0] + ((rc2 == rk) ? c->lU1 : c->lU2) : -INFINITY;
+    else lk = (dk2 == dk + 1 && rk2 == rk) ? hk[1] : -INFINITY;
+  }
+  return (lm + lc) + lk;
+}
+
+/* CaseControlProposal: proposal slot s of ancestor a (slots 0..2K-1 from _xi,
+ * 2K.. from proposal_fn_non_resampled). */
+static uint64_t tg_xi(int K, uint64_t a, int s) {
+  const int m = hyg_st_m(a), dc = hyg_st_dc(a), rc = hyg_st_rc(a), dk = hyg_st_dk(a), rk = hyg_st_rk(a);
+  if (s == 0) return hyg_st_pack(m, dc + 1, rc, dk + 1, rk);
+  if (s < K) { /* loop_fn_control_split1/2: control regimes except r_case */
+    const int r = (s - 1 < rk) ? s - 1 : s;
+    return hyg_st_pack(0, 1, r, dk + 1, rk);
+  }
+  if (s < 2 * K - 1) { /* loop_fn_case_split1/2: case regimes except r_ctrl */
+    const int q = s - K;
+    const int r = (q < rc) ? q : q + 1;
+    return hyg_st_pack(0, dc + 1, rc, 1, r);
+  }
+  if (s == 2 * K - 1) { /* merged_state_case_cp */
+    const int d = (m == 0) ? dc + 1 : 0;
+    return hyg_st_pack(1, d, rc, d, rc);
+  }
+  const int j = s - 2 * K, i = j / K, jj = j % K; /* loop_fn_two_change_points */
+  return hyg_st_pack(i == jj, 1, i, 1, jj);
+}
+
+/* ------------------------------------------------------------ history */
+/* What step t keeps for the backward pass: the ancestors resampled at t
+ * (their states and previous weights) and the scalars of the weight update.
+ * The N_t particles of step t are a deterministic function of this record
+ * (proposal + weight formula), so they are regenerated instead of stored. */
+enum { MODE_KEEP = 0, MODE_OPTIMAL = 1, MODE_UNBIASED = 2, MODE_INIT = 3 };
+typedef struct {
+  int mode, n_par;
+  float log_c;
+  double lse;
+  int r_ph; /* t = 0 only */
+} step_rec;
+
+typedef struct {
+  const oracle_model* om;
+  const double* E;
+  int T;
+  step_rec* rec;
+  uint64_t* par_state; /* [T][M] */
+  double* par_w;       /* [T][M] */
+} chain_ctx;
+
+/* particles of step t: st[n], W[n] for n < return value */
+static int gen_particles(const chain_ctx* cx, int t, uint64_t* st, double* W) {
+  const hyg_tg_consts* c = &cx->om->c;
+  const int K = c->K;
+  const double* Et = cx->E + (size_t)t * 2 * K;
+  const step_rec* r = &cx->rec[t];
+  if (r->mode == MODE_INIT) {
+    /* _filter_first_step: K^2 candidates, prior = transition from the phantom */
+    for (int i = 0; i < K; ++i)
+      for (int j = 0; j < K; ++j) {
+        const int n = i * K + j;
+        st[n] = hyg_st_pack(i == j, 1, i, 1, j);
+        const double obs = Et[i] + Et[K + j];
+        const double tr = (i == j) ? c->lPc[r->r_ph * K + i] : -INFINITY;
+        W[n] = obs + tr;
+      }
+    return K * K;
+  }
+  const int np = r->n_par;
+  const uint64_t* ps = cx->par_state + (size_t)t * c->M;
+  const double* pw = cx->par_w + (size_t)t * c->M;
+  for (int s = 0; s < c->I; ++s)
+    for (int a = 0; a < np; ++a) {
+      const int n = s * np + a;
+      const uint64_t x = tg_xi(K, ps[a], s);
+      st[n] = x;
+      const double tr = tg_trans(cx->om, ps[a], x);
+      if (!hyg_isfinite(tr)) { W[n] = -INFINITY; continue; }
+      const double lg = tr + (Et[hyg_st_rc(x)] + Et[K + hyg_st_rk(x)]);
+      double w;
+      if (r->mode == MODE_KEEP) {
+        w = pw[a] + lg;
+      } else if (r->mode == MODE_UNBIASED) {
+        w = (-c->log_M + r->lse) + lg;
+      } else {
+        const double v = (double)r->log_c + (pw[a] - r->lse);
+        w = (pw[a] + lg) - (v < 0.0 ? v : 0.0);
+      }
+      W[n] = w;
+    }
+  return c->I * np;
+}
+
+/* ---------------------------------------------------- sums and draws */
+/* logsumexp with the exact F=100 mass sum; returns max via *mx, log S via *logS */
+static void lse_exact(const double* W, int N, double* mx_out, double* logS_out) {
+  double mx = -INFINITY;
+  for (int n = 0; n < N; ++n) if (W[n] > mx) mx = W[n];
+  hyg_u128 S = hyg_u128_zero();
+  if (mx != -INFINITY)
+    for (int n = 0; n < N; ++n) S = hyg_u128_add(S, hyg_fix100(hyg_exp(W[n] - mx)));
+  *mx_out = mx;
+  *logS_out = hyg_log(hyg_u128_to_f64(S, 100));
+}
+
+/* tfd.Categorical(logits).sample(): first n with cdf_n > floor(u * total) */
+static int categorical(const double* l, int N, uint64_t r) {
+  double lmax = -INFINITY;
+  for (int n = 0; n < N; ++n) if (l[n] > lmax) lmax = l[n];
+  if (lmax == -INFINITY) return -1;
+  hyg_u128 total = hyg_u128_zero();
+  for (int n = 0; n < N; ++n) total = hyg_u128_add(total, hyg_fix100(hyg_exp(l[n] - lmax)));
+  const hyg_u128 target = hyg_scale_target(r, total);
+  hyg_u128 cdf = hyg_u128_zero();
+  for (int n = 0; n < N; ++n) {
+    cdf = hyg_u128_add(cdf, hyg_fix100(hyg_exp(l[n] - lmax)));
+    if (hyg_u128_lt(target, cdf)) return n;
+  }
+  return N - 1; /* unreachable: target < total */
+}
+
+static uint64_t sort_key(float x, int idx) {
+  uint32_t u = hyg_f32_bits(x);
+  if (u == 0x80000000u) u = 0; /* -0 == +0 */
+  const uint32_t ord = (u >> 31) ? ~u : (u | 0x80000000u);
+  return ((uint64_t)(~ord) << 32) | (uint32_t)idx;
+}
+static int cmp_u64(const void* a, const void* b) {
+  const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+/* SystematicResampling (resampling_functions.py:56-69) on the residual
+ * sorted[K:]: T_j = (j + U)/L in float32, Q = exact cumulative residual mass
+ * / residual total; parents[j] = first i with T_j <= Q_i (unfilled -> 0). */
+static void systematic_residual(const float* mass_sorted, int K, int Np, int L, float U, int* out) {
+  hyg_u192 R = hyg_u192_zero();
+  for (int p = K; p < Np; ++p) R = hyg_u192_add(R, hyg_fix149f(mass_sorted[p]));
+  const double Rd = hyg_u192_to_f64(R);
+  for (int j = 0; j < L; ++j) out[j] = 0;
+  int i = 0, j = 0;
+  hyg_u192 C = hyg_fix149f(mass_sorted[K]);
+  const int len = Np - K;
+  while (j < L && i < len) {
+    const float Tj = ((float)j + U) / (float)L;
+    const double Qi = hyg_u192_to_f64(C) / Rd;
+    if ((double)Tj <= Qi) {
+      out[j] = i;
+      ++j;
+    } else {
+      ++i;
+      if (i < len) C = hyg_u192_add(C, hyg_fix149f(mass_sorted[K + i]));
+    }
+  }
+}
+
+/* One forward step t >= 1: resample the particles of step t-1 (st, W, N) and
+ * fill rec[t], par_state[t], par_w[t]. Returns HYG_OK or HYG_ENUMERIC. */
+static int resample_step(chain_ctx* cx, int t, const uint64_t* st, const double* W, int N, uint64_t seed,
+                         uint64_t chain_id, float* lw32, uint64_t* keys, float* mass, hyg_u192* revcum,
+                         int* parents) {
+  const hyg_tg_consts* c = &cx->om->c;
+  const int M = c->M;
+  step_rec* r = &cx->rec[t];
+  double mx, logS;
+  lse_exact(W, N, &mx, &logS);
+  if (mx == -INFINITY) return HYG_ENUMERIC;
+  r->lse = logS + mx;
+  r->log_c = 0.0f;
+  int count = 0;
+  for (int n = 0; n < N; ++n) count += (W[n] > -INFINITY);
+  int np = 0;
+  if (count <= M) {
+    /* keep every particle with non-zero weight (filter_and_smoother_algorithm.py:207-209) */
+    r->mode = MODE_KEEP;
+    for (int n = 0; n < N; ++n) if (W[n] > -INFINITY) parents[np++] = n;
+  } else {
+    for (int n = 0; n < N; ++n) lw32[n] = (float)((W[n] - mx) - logS); /* log_softmax, cast f32 */
+    int unbiased = 0;
+    if (c->optimal) {
+      /* OptimalFiniteState (resampling_functions.py:7-52) */
+      for (int n = 0; n < N; ++n) keys[n] = sort_key(lw32[n], n);
+      qsort(keys, (size_t)N, sizeof(uint64_t), cmp_u64);
+      for (int p = 0; p < N; ++p) mass[p] = hyg_expf(lw32[(int)(uint32_t)keys[p]]);
+      revcum[N] = hyg_u192_zero();
+      for (int p = N - 1; p >= 0; --p) revcum[p] = hyg_u192_add(revcum[p + 1], hyg_fix149f(mass[p]));
+      int a = 0, b = -1;
+      float lc = -1.0f;
+      while (a != b && a < N && a < M) {
+        const float l1 = hyg_logf((float)(M - a));
+        const double rv = hyg_u192_to_f64(revcum[a]);
+        const float l2 = (rv == 0.0) ? HYG_NINFF : (float)hyg_log(rv);
+        const float cnew = l1 - l2;
+        int cnt = 0;
+        for (int p = a; p < N; ++p) cnt += ((float)(cnew + lw32[(int)(uint32_t)keys[p]]) > 0.0f);
+        b = a;
+        a = a + cnt;
+        lc = cnew;
+      }
+      int K = b;
+      float log_c = lc;
+      if (K >= N) { K = N; log_c = HYG_NINFF; }
+      if (!hyg_isfinitef(log_c)) {
+        unbiased = 1;
+      } else {
+        const int L = M - K;
+        for (int p = 0; p < K; ++p) parents[p] = (int)(uint32_t)keys[p];
+        if (L > 0) {
+          int sys[1 << 12];
+          int* sp = (L <= (1 << 12)) ? sys : (int*)malloc(sizeof(int) * L);
+          const float U = hyg_u01f(hyg_rand64(seed, chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)t, 0));
+          systematic_residual(mass, K, N, L, U, sp);
+          for (int j = 0; j < L; ++j) parents[K + j] = (int)(uint32_t)keys[K + sp[j]];
+          if (sp != sys) free(sp);
+        }
+        np = M;
+        r->mode = MODE_OPTIMAL;
+        r->log_c = log_c;
+      }
+    } else {
+      unbiased = 1; /* UnbiasedResampling (resampling_functions.py:71-79) */
+      if (!c->multinomial) {
+        /* systematic over all particles */
+        hyg_u192 R = hyg_u192_zero();
+        for (int n = 0; n < N; ++n) { mass[n] = hyg_expf(lw32[n]); R = hyg_u192_add(R, hyg_fix149f(mass[n])); }
+        (void)R;
+        const float U = hyg_u01f(hyg_rand64(seed, chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)t, 0));
+        systematic_residual(mass, 0, N, M, U, parents);
+        np = M;
+        r->mode = MODE_UNBIASED;
+        unbiased = 0;
+      }
+    }
+    if (unbiased) {
+      /* tfd.Categorical(logits=log_weights).sample(M) (resampling_functions.py:46) */
+      double* l = (double*)malloc(sizeof(double) * N);
+      for (int n = 0; n < N; ++n) l[n] = (double)lw32[n];
+      for (int j = 0; j < M; ++j)
+        parents[j] = categorical(l, N, hyg_rand64(seed, chain_id, HYG_RNG_MULTINOMIAL, (uint64_t)t, (uint64_t)j));
+      free(l);
+      np = M;
+      r->mode = MODE_UNBIASED;
+      r->log_c = 0.0f;
+    }
+  }
+  r->n_par = np;
+  for (int a = 0; a < np; ++a) {
+    cx->par_state[(size_t)t * M + a] = st[parents[a]];
+    cx->par_w[(size_t)t * M + a] = W[parents[a]];
+  }
+  return HYG_OK;
+}
+
+/* Whole chain: filter forward over T sites, then backward simulation of B
+ * trajectories. E is the emission table [T][2K]. Outputs (host, untrimmed):
+ * merged[T][B], control[T][B][2], kase[T][B][2] int16; split[T], regime[T][2K]
+ * f32; *log_z; final_w[Nmax] (may be NULL). n_parents_out[T] (may be NULL)
+ * receives the number of resampled ancestors of every step (debug). */
+int oracle_tg_chain(const hyg_tg_params* p, const double* E, int T, uint64_t seed, uint64_t chain_id,
+                    int16_t* merged, int16_t* control, int16_t* kase, float* split, float* regime,
+                    double* log_z, double* final_w, int32_t* mode_out) {
+  if (T < 1 || T >= HYG_DMAX - 2) return HYG_EINVAL;
+  oracle_model om;
+  int rc = om_init(&om, p, T + 2);
+  if (rc) return rc;
+  const hyg_tg_consts* c = &om.c;
+  const int K = c->K, M = c->M, B = c->B, Nmax = c->Nmax;
+  chain_ctx cx;
+  cx.om = &om;
+  cx.E = E;
+  cx.T = T;
+  cx.rec = (step_rec*)calloc((size_t)T, sizeof(step_rec));
+  cx.par_state = (uint64_t*)calloc((size_t)T * M, sizeof(uint64_t));
+  cx.par_w = (double*)calloc((size_t)T * M, sizeof(double));
+  uint64_t* st = (uint64_t*)malloc(sizeof(uint64_t) * Nmax);
+  double* W = (double*)malloc(sizeof(double) * Nmax);
+  float* lw32 = (float*)malloc(sizeof(float) * Nmax);
+  uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * Nmax);
+  float* mass = (float*)malloc(sizeof(float) * Nmax);
+  hyg_u192* revcum = (hyg_u192*)malloc(sizeof(hyg_u192) * (Nmax + 1));
+  int* parents = (int*)malloc(sizeof(int) * (M > Nmax ? M : Nmax));
+  double* logits = (double*)malloc(sizeof(double) * Nmax);
+  uint64_t* X = (uint64_t*)malloc(sizeof(uint64_t) * B);
+  if (!cx.rec || !cx.par_state || !cx.par_w || !st || !W || !lw32 || !keys || !mass || !revcum || !parents ||
+      !logits || !X) {
+    rc = HYG_ENOMEM;
+    goto done;
+  }
+  /* ---- forward filter (filter_and_smoother_algorithm.py:60-109) */
+  cx.rec[0].mode = MODE_INIT;
+  cx.rec[0].r_ph = (int)hyg_mulhi64(hyg_rand64(seed, chain_id, HYG_RNG_PHANTOM, 0, 0), (uint64_t)K);
+  int N = gen_particles(&cx, 0, st, W);
+  for (int t = 1; t < T; ++t) {
+    rc = resample_step(&cx, t, st, W, N, seed, chain_id, lw32, keys, mass, revcum, parents);
+    if (rc) goto done;
+    if (mode_out) mode_out[t] = cx.rec[t].mode * 65536 + cx.rec[t].n_par;
+    N = gen_particles(&cx, t, st, W);
+  }
+  if (mode_out) mode_out[0] = MODE_INIT * 65536;
+  {
+    double mx, logS;
+    lse_exact(W, N, &mx, &logS);
+    if (mx == -INFINITY) { rc = HYG_ENUMERIC; goto done; }
+    *log_z = logS + mx;
+    if (final_w) {
+      for (int n = 0; n < Nmax; ++n) final_w[n] = (n < N) ? W[n] : -INFINITY;
+    }
+  }
+  /* ---- backward simulation (filter_and_smoother_algorithm.py:368-447) */
+  for (int t = T - 1; t >= 0; --t) {
+    N = gen_particles(&cx, t, st, W);
+    for (int b = 0; b < B; ++b) {
+      const uint64_t rnd = hyg_rand64(seed, chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
+      int idx;
+      if (t == T - 1) {
+        idx = categorical(W, N, rnd);
+      } else {
+        for (int n = 0; n < N; ++n) {
+          const double f = hyg_isfinite(W[n]) ? tg_trans(&om, st[n], X[b]) : -INFINITY;
+          logits[n] = (hyg_isfinite(f) && hyg_isfinite(W[n])) ? f + W[n] : -INFINITY;
+        }
+        idx = categorical(logits, N, rnd);
+      }
+      if (idx < 0) { rc = HYG_ENUMERIC; goto done; }
+      parents[b] = idx;
+    }
+    int n_split = 0, nc[HYG_KMAX], nk[HYG_KMAX];
+    for (int r = 0; r < K; ++r) nc[r] = nk[r] = 0;
+    for (int b = 0; b < B; ++b) {
+      const uint64_t x = st[parents[b]];
+      X[b] = x;
+      const size_t o = (size_t)t * B + b;
+      merged[o] = (int16_t)hyg_st_m(x);
+      control[2 * o + 0] = (int16_t)hyg_st_dc(x);
+      control[2 * o + 1] = (int16_t)hyg_st_rc(x);
+      kase[2 * o + 0] = (int16_t)hyg_st_dk(x);
+      kase[2 * o + 1] = (int16_t)hyg_st_rk(x);
+      n_split += (hyg_st_m(x) == 0);
+      nc[hyg_st_rc(x)]++;
+      nk[hyg_st_rk(x)]++;
+    }
+    split[t] = (float)n_split / (float)B;
+    for (int r = 0; r < K; ++r) {
+      regime[(size_t)t * 2 * K + r] = (float)nc[r] / (float)B;
+      regime[(size_t)t * 2 * K + K + r] = (float)nk[r] / (float)B;
+    }
+  }
+  rc = HYG_OK;
+done:
+  free(cx.rec); free(cx.par_state); free(cx.par_w); free(st); free(W); free(lw32); free(keys); free(mass);
+  free(revcum); free(parents); free(logits); free(X);
+  om_free(&om);
+  return rc;
+}
+
+/* ---------------------------------------------------- exported helpers */
+/* for tests: the transition density between two packed states (t >= 1) */
+double oracle_tg_trans(const hyg_tg_params* p, int max_duration, uint64_t prev, uint64_t next) {
+  oracle_model om;
+  if (om_init(&om, p, max_duration)) return NAN;
+  const double v = tg_trans(&om, prev, next);
+  om_free(&om);
+  return v;
+}
+uint64_t oracle_tg_xi(int K, uint64_t a, int s) { return tg_xi(K, a, s); }
+/* for tests: hazard table (log rho, log 1-rho) for d in [0, n) */
+int oracle_tg_hazard(const hyg_tg_params* p, int g, int r, int n, double* out) {
+  oracle_model om;
+  int rc = om_init(&om, p, n + 2);
+  if (rc) return rc;
+  for (int d = 0; d < n; ++d) {
+    const double* h = om_hz(&om, g, r, d);
+    out[2 * d] = h[0];
+    out[2 * d + 1] = h[1];
+  }
+  om_free(&om);
+  return HYG_OK;
+}
+int oracle_tg_consts(const hyg_tg_params* p, hyg_tg_consts* out) { return hyg_tg_derive(p, out); }
+/* arithmetic primitives for tests/test_arith.py */
+double oracle_exp(double x) { return hyg_exp(x); }
+double oracle_log(double x) { return hyg_log(x); }
+void oracle_philox(uint64_t c0, uint64_t c1, uint64_t c2, uint64_t c3, uint64_t k0, uint64_t k1, uint64_t* out) {
+  const hyg_ph4 r = hyg_philox4x64(c0, c1, c2, c3, k0, k1);
+  for (int i = 0; i < 4; ++i) out[i] = r.v[i];
+}
+double oracle_u192_roundtrip(float m) { return hyg_u192_to_f64(hyg_fix149f(m)); }
+double oracle_u128_roundtrip(double e) { return hyg_u128_to_f64(hyg_fix100(e), 100); }
+int oracle_sizeof_params(void) { return (int)sizeof(hyg_tg_params); }
+int oracle_sizeof_consts(void) { return (int)sizeof(hyg_tg_consts); }

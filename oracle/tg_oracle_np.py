@@ -1,0 +1,393 @@
+"""Independent pure-Python restatement of the two-group chain (TEST INFRASTRUCTURE).
+
+A second, language-independent implementation of the same reference algorithm
+as oracle/tg_oracle.c, used only by tests to cross-check the C oracle bit for
+bit on small chains (T ~ 100, M ~ 10). It re-implements the arithmetic
+contract of include/hyg_arith.h itself (Python floats are IEEE doubles with no
+FMA; numpy float32 scalars give IEEE single ops; Python ints make the exact
+mass sums trivially exact) and reads only the model TABLES from the C side
+(constants and hazard), which tests/test_model_tables.py pins against scipy.
+
+Reference (src/two_group/hygeia): filter_and_smoother_algorithm.py:141-288
+(forward steps), 368-447 (backward simulation); resampling_functions.py:7-69;
+case_control_regime_model.py:80-231; case_control_distributions.py:138-291;
+case_control_proposal_mappings.py:11-216; run_inference_two_groups.py:233-296.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+NINF = float("-inf")
+M64 = (1 << 64) - 1
+
+# ------------------------------------------------------------ arithmetic
+_LN2_HI = 6.93147180369123816490e-01
+_LN2_LO = 1.90821492927058770002e-10
+_INV_LN2 = 1.44269504088896338700e+00
+_EXP_C = [1.6059043836821614599e-10, 2.0876756987868098979e-09, 2.5052108385441718775e-08,
+          2.7557319223985890653e-07, 2.7557319223985890653e-06, 2.4801587301587301566e-05,
+          1.9841269841269841253e-04, 1.3888888888888888889e-03, 8.3333333333333332177e-03,
+          4.1666666666666664354e-02, 1.6666666666666665741e-01, 0.5, 1.0, 1.0]
+_LOG_C = [0.08695652173913043478, 0.09523809523809523810, 0.10526315789473684211,
+          0.11764705882352941176, 0.13333333333333333333, 0.15384615384615384615,
+          0.18181818181818181818, 0.22222222222222222222, 0.28571428571428571429,
+          0.40000000000000000000, 0.66666666666666666667]
+
+
+def _pow2(e: int) -> float:
+    return math.ldexp(1.0, e)
+
+
+def det_exp(x: float) -> float:
+    if x != x:
+        return x
+    if x > 709.782712893383973096:
+        return math.inf
+    if x < -745.13321910194110842:
+        return 0.0
+    kd = math.floor(x * _INV_LN2 + 0.5)
+    k = int(kd)
+    hi = x - kd * _LN2_HI
+    lo = kd * _LN2_LO
+    r = hi - lo
+    p = _EXP_C[0]
+    for c in _EXP_C[1:]:
+        p = c + r * p
+    if k > 1023:
+        return (p * 2.0) * _pow2(k - 1)
+    if k >= -1021:
+        return p * _pow2(k)
+    return (p * _pow2(k + 54)) * _pow2(-54)
+
+
+def det_log(x: float) -> float:
+    if x != x or x < 0.0:
+        return math.nan
+    if x == 0.0:
+        return NINF
+    if x == math.inf:
+        return x
+    m, e = math.frexp(x)  # x = m 2^e, m in [0.5, 1)
+    m *= 2.0
+    e -= 1
+    if m > 1.41421356237309504880:
+        m *= 0.5
+        e += 1
+    f = m - 1.0
+    s = f / (2.0 + f)
+    z = s * s
+    R = _LOG_C[0]
+    for c in _LOG_C[1:]:
+        R = c + z * R
+    R = z * R
+    hfsq = 0.5 * f * f
+    l1p = f - (hfsq - s * (hfsq + R))
+    ed = float(e)
+    return ed * _LN2_HI + (ed * _LN2_LO + l1p)
+
+
+def f32(x) -> np.float32:
+    return np.float32(x)
+
+
+def det_expf(x: np.float32) -> np.float32:
+    return np.float32(det_exp(float(x)))
+
+
+def det_logf(x: np.float32) -> np.float32:
+    return np.float32(det_log(float(x)))
+
+
+def fix100(e: float) -> int:
+    """floor(e * 2^100) exactly."""
+    if not e > 0.0:
+        return 0
+    m, ex = math.frexp(e)  # e = m 2^ex, m in [0.5,1): mant = m*2^53
+    mant = int(m * (1 << 53))
+    sh = ex - 53 + 100
+    return mant << sh if sh >= 0 else mant >> (-sh)
+
+
+def fix149f(m: np.float32) -> int:
+    """exact m * 2^149 for an f32 m in [0, 1]."""
+    v = float(m)
+    if v <= 0.0:
+        return 0
+    fr, ex = math.frexp(v)
+    mant = int(fr * (1 << 24))
+    sh = ex - 24 + 149
+    if sh >= 0:
+        return mant << sh
+    assert mant & ((1 << -sh) - 1) == 0  # f32 subnormals are multiples of 2^-149
+    return mant >> (-sh)
+
+
+def int_to_f64(V: int, scale: int) -> float:
+    """top 53 bits (truncated) of V, times 2^-scale."""
+    if V == 0:
+        return 0.0
+    p = V.bit_length() - 1
+    if p <= 52:
+        return float(V) * _pow2(-scale)
+    sh = p - 52
+    return float(V >> sh) * _pow2(sh - scale)
+
+
+def philox4x64(c, k):
+    c = list(c)
+    k0, k1 = k
+    for _ in range(10):
+        p0 = 0xD2E7470EE14C6C93 * c[0]
+        p1 = 0xCA5A826395121157 * c[2]
+        hi0, lo0 = (p0 >> 64) & M64, p0 & M64
+        hi1, lo1 = (p1 >> 64) & M64, p1 & M64
+        c = [hi1 ^ c[1] ^ k0, lo1, hi0 ^ c[3] ^ k1, lo0]
+        k0 = (k0 + 0x9E3779B97F4A7C15) & M64
+        k1 = (k1 + 0xBB67AE8584CAA73B) & M64
+    return c
+
+
+RNG_PHANTOM, RNG_SYSTEMATIC, RNG_MULTINOMIAL, RNG_BACKWARD = 1, 2, 3, 4
+
+
+def rand64(seed, chain, stream, step, index):
+    return philox4x64((stream, step, index >> 2, 0), (seed, chain))[index & 3]
+
+
+def u01f(r: int) -> np.float32:
+    return np.float32((r >> 40) * 5.9604644775390625e-08)
+
+
+def categorical(logits, r: int) -> int:
+    lmax = max(logits)
+    if lmax == NINF:
+        return -1
+    masses = [fix100(det_exp(l - lmax)) for l in logits]
+    total = sum(masses)
+    target = (r * total) >> 64
+    cdf = 0
+    for n, q in enumerate(masses):
+        cdf += q
+        if target < cdf:
+            return n
+    return len(logits) - 1
+
+
+# ---------------------------------------------------------------- model
+class Model:
+    def __init__(self, consts, hazard_rows, dcap):
+        """consts: binding.TgConsts; hazard_rows[(g, r)] = array [dcap, 2]"""
+        c = consts
+        self.K, self.u, self.M, self.B, self.I = c.K, c.u, c.M, c.B, c.I
+        self.lPc = [c.lPc[i] for i in range(c.K * c.K)]
+        self.lPm = [c.lPm[i] for i in range(4)]
+        self.lU1, self.lU2, self.log_M = c.lU1, c.lU2, c.log_M
+        self.hz = hazard_rows
+        self.dcap = dcap
+
+    def haz(self, g, r, d):
+        d = min(max(d, 0), self.dcap - 1)
+        row = self.hz[(g, r)]
+        return float(row[d, 0]), float(row[d, 1])
+
+    def trans(self, prev, nxt):
+        m, dc, rc, dk, rk = prev
+        m2, dc2, rc2, dk2, rk2 = nxt
+        K = self.K
+        if min(dk, dc) >= self.u:
+            lm = self.lPm[m * 2 + m2]
+        else:
+            lm = 0.0 if m2 == m else NINF
+        lr, l1 = self.haz(0, rc, dc)
+        if dc2 == 1:
+            lc = lr + self.lPc[rc * K + rc2]
+        else:
+            lc = l1 if (dc2 == dc + 1 and rc2 == rc) else NINF
+        if m2 == 1:
+            lk = 0.0 if (rk2 == rc2 and dk2 == dc2) else NINF
+        elif m == 1 and dc2 != 1:
+            lk = self.lU1 if (dk2 == 1 and rk2 != rc2) else NINF
+        elif rc2 == rk and m == 0:
+            lk = self.lU1 if (dk2 == 1 and rk2 != rc2) else NINF
+        else:
+            kr, k1 = self.haz(1, rk, dk)
+            if dk2 == 1:
+                lk = kr + (self.lU1 if rc2 == rk else self.lU2) if (rk2 != rc2 and rk2 != rk) else NINF
+            else:
+                lk = k1 if (dk2 == dk + 1 and rk2 == rk) else NINF
+        return (lm + lc) + lk
+
+    def xi(self, a, s):
+        m, dc, rc, dk, rk = a
+        K = self.K
+        if s == 0:
+            return (m, dc + 1, rc, dk + 1, rk)
+        if s < K:
+            r = s - 1 if s - 1 < rk else s
+            return (0, 1, r, dk + 1, rk)
+        if s < 2 * K - 1:
+            q = s - K
+            r = q if q < rc else q + 1
+            return (0, dc + 1, rc, 1, r)
+        if s == 2 * K - 1:
+            d = dc + 1 if m == 0 else 0
+            return (1, d, rc, d, rc)
+        j = s - 2 * K
+        i, jj = divmod(j, K)
+        return (int(i == jj), 1, i, 1, jj)
+
+
+def _sort_key(x: np.float32, idx: int) -> int:
+    u = int(np.array(x, dtype=np.float32).view(np.uint32))
+    if u == 0x80000000:
+        u = 0
+    ord_ = (~u & 0xFFFFFFFF) if (u >> 31) else (u | 0x80000000)
+    return ((~ord_ & 0xFFFFFFFF) << 32) | idx
+
+
+def run_chain(model: Model, E: np.ndarray, seed: int, chain: int):
+    K, M, B, I = model.K, model.M, model.B, model.I
+    T = E.shape[0]
+    recs = []
+
+    def particles(t):
+        rec = recs[t]
+        Et = [float(v) for v in E[t]]
+        st, W = [], []
+        if rec["mode"] == "init":
+            rph = rec["r_ph"]
+            for i in range(K):
+                for j in range(K):
+                    st.append((int(i == j), 1, i, 1, j))
+                    tr = model.lPc[rph * K + i] if i == j else NINF
+                    W.append((Et[i] + Et[K + j]) + tr)
+            return st, W
+        ps, pw = rec["ps"], rec["pw"]
+        np_ = len(ps)
+        for s in range(I):
+            for a in range(np_):
+                x = model.xi(ps[a], s)
+                st.append(x)
+                tr = model.trans(ps[a], x)
+                if not math.isfinite(tr):
+                    W.append(NINF)
+                    continue
+                lg = tr + (Et[x[2]] + Et[K + x[4]])
+                if rec["mode"] == "keep":
+                    w = pw[a] + lg
+                elif rec["mode"] == "unbiased":
+                    w = (-model.log_M + rec["lse"]) + lg
+                else:
+                    v = float(rec["log_c"]) + (pw[a] - rec["lse"])
+                    w = (pw[a] + lg) - (v if v < 0.0 else 0.0)
+                W.append(w)
+        return st, W
+
+    def lse_exact(W):
+        mx = max(W)
+        if mx == NINF:
+            return mx, NINF
+        S = sum(fix100(det_exp(w - mx)) for w in W)
+        return mx, det_log(int_to_f64(S, 100))
+
+    rph = (rand64(seed, chain, RNG_PHANTOM, 0, 0) * K) >> 64
+    recs.append({"mode": "init", "r_ph": rph})
+    st, W = particles(0)
+    for t in range(1, T):
+        mx, logS = lse_exact(W)
+        if mx == NINF:
+            raise FloatingPointError("all weights -inf")
+        lse = logS + mx
+        N = len(W)
+        nz = [n for n in range(N) if W[n] > NINF]
+        rec = {"lse": lse, "log_c": np.float32(0.0)}
+        if len(nz) <= M:
+            parents = nz
+            rec["mode"] = "keep"
+        else:
+            lw32 = [np.float32((w - mx) - logS) for w in W]
+            keys = sorted(_sort_key(lw32[n], n) for n in range(N))
+            order = [k & 0xFFFFFFFF for k in keys]
+            mass = [det_expf(lw32[n]) for n in order]
+            ints = [fix149f(m) for m in mass]
+            revcum = [0] * (N + 1)
+            for p in range(N - 1, -1, -1):
+                revcum[p] = revcum[p + 1] + ints[p]
+            a, b, lc = 0, -1, np.float32(-1.0)
+            while a != b and a < N and a < M:
+                l1 = det_logf(np.float32(M - a))
+                rv = int_to_f64(revcum[a], 149)
+                l2 = np.float32(NINF) if rv == 0.0 else np.float32(det_log(rv))
+                with np.errstate(invalid="ignore"):
+                    cnew = np.float32(l1 - l2)
+                    cnt = sum(1 for p in range(a, N) if np.float32(cnew + lw32[order[p]]) > np.float32(0.0))
+                b, a, lc = a, a + cnt, cnew
+            Kk, log_c = b, lc
+            if Kk >= N:
+                Kk, log_c = N, np.float32(NINF)
+            if not np.isfinite(log_c):
+                l = [float(x) for x in lw32]
+                parents = [categorical(l, rand64(seed, chain, RNG_MULTINOMIAL, t, j)) for j in range(M)]
+                rec["mode"] = "unbiased"
+            else:
+                L = M - Kk
+                parents = order[:Kk]
+                R = revcum[Kk]
+                Rd = int_to_f64(R, 149)
+                U = u01f(rand64(seed, chain, RNG_SYSTEMATIC, t, 0))
+                sys_ = [0] * L
+                i, j, C = 0, 0, ints[Kk]
+                ln = N - Kk
+                while j < L and i < ln:
+                    Tj = np.float32((np.float32(j) + U) / np.float32(L))
+                    if float(Tj) <= int_to_f64(C, 149) / Rd:
+                        sys_[j] = i
+                        j += 1
+                    else:
+                        i += 1
+                        if i < ln:
+                            C += ints[Kk + i]
+                parents = parents + [order[Kk + s] for s in sys_]
+                rec["mode"] = "optimal"
+                rec["log_c"] = log_c
+        rec["ps"] = [st[q] for q in parents]
+        rec["pw"] = [W[q] for q in parents]
+        recs.append(rec)
+        st, W = particles(t)
+    mx, logS = lse_exact(W)
+    log_z = logS + mx
+    final_w = list(W)
+    merged = np.zeros((T, B), np.int16)
+    control = np.zeros((T, B, 2), np.int16)
+    case = np.zeros((T, B, 2), np.int16)
+    X = [None] * B
+    for t in range(T - 1, -1, -1):
+        st, W = particles(t)
+        idx = []
+        for b in range(B):
+            r = rand64(seed, chain, RNG_BACKWARD, t, b)
+            if t == T - 1:
+                q = categorical(W, r)
+            else:
+                logits = []
+                for n in range(len(W)):
+                    f = model.trans(st[n], X[b]) if math.isfinite(W[n]) else NINF
+                    logits.append(f + W[n] if (math.isfinite(f) and math.isfinite(W[n])) else NINF)
+                q = categorical(logits, r)
+            if q < 0:
+                raise FloatingPointError("backward kernel all -inf")
+            idx.append(q)
+        for b in range(B):
+            x = st[idx[b]]
+            X[b] = x
+            merged[t, b] = x[0]
+            control[t, b] = (x[1], x[2])
+            case[t, b] = (x[3], x[4])
+    split = (merged == 0).sum(1).astype(np.float32) / np.float32(B)
+    reg = np.concatenate([np.stack([(control[:, :, 1] == r).sum(1) for r in range(K)], 1),
+                          np.stack([(case[:, :, 1] == r).sum(1) for r in range(K)], 1)], 1)
+    regime = reg.astype(np.float32) / np.float32(B)
+    return {"merged": merged, "control": control, "case": case, "split_probs": split,
+            "regime_probs": regime, "log_z": log_z, "final_log_weights": final_w}
