@@ -1,0 +1,296 @@
+// capi.cpp -- the C ABI of include/hygeia_amd.h: model construction (host
+// tables, upload), workspace planning, chain descriptors, launches. Compiled by
+// hipcc into hygeia_amd/lib/libhygeia_amd.so together with tg_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hyg_arith.h"
+#include "../../include/hygeia_amd.h"
+#include "tg_common.h"
+
+using namespace hyg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+bool have_device() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return n > 0;
+}
+
+template <typename T>
+hipError_t dmalloc_copy(T** dst, const T* src, size_t count) {
+  hipError_t e = hipMalloc((void**)dst, sizeof(T) * (count ? count : 1));
+  if (e != hipSuccess) return e;
+  if (count) e = hipMemcpy(*dst, src, sizeof(T) * count, hipMemcpyHostToDevice);
+  return e;
+}
+
+}  // namespace
+
+struct hyg_tg_model {
+  hyg_tg_consts c{};
+  int32_t dcap = 0;
+  int32_t nmax_reads = 0;
+  int32_t max_duration = 0;
+  std::vector<double> hz, lf, lg, cst;
+  bool on_device = false;
+  int device = -1;
+  hyg_tg_consts* d_consts = nullptr;
+  double* d_hz = nullptr;
+  double* d_lf = nullptr;
+  double* d_lg = nullptr;
+  double* d_cst = nullptr;
+
+  ModelDev dev() const {
+    ModelDev m{};
+    m.consts = d_consts;
+    m.hz = d_hz;
+    m.dcap = dcap;
+    m.nmax_reads = nmax_reads;
+    m.lf = d_lf;
+    m.lg = d_lg;
+    m.cst = d_cst;
+    return m;
+  }
+};
+
+extern "C" {
+
+const char* hyg_version(void) { return "hygeia_amd 0.1.0 (gfx950)"; }
+
+const char* hyg_last_error(void) { return g_err.c_str(); }
+
+int hyg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+void hyg_tg_params_default(hyg_tg_params* p) {
+  std::memset(p, 0, sizeof(*p));
+  const double mu[6] = {0.95, 0.05, 0.80, 0.20, 0.50, 0.50};
+  const double sg[6] = {0.05, 0.05, 0.1, 0.1, 0.1, 0.2886751};
+  p->n_regimes = 6;
+  p->minimum_duration = 3;
+  p->num_resampled_ancestors = 50;
+  p->num_samples_backward = 25;
+  p->optimal_resampling = 1;
+  p->multinomial = 0;
+  for (int i = 0; i < 6; ++i) {
+    p->mu[i] = mu[i];
+    p->sigma[i] = sg[i];
+  }
+  // uniform off-diagonal transitions, omega = 0.8
+  p->theta_len = 36;
+  for (int i = 0; i < 30; ++i) p->theta[i] = 0.0;
+  for (int i = 30; i < 36; ++i) p->theta[i] = std::log(0.8 / 0.2);
+  p->omega_case = 0.8;
+  p->merge_log_prob = std::log(0.1);
+  p->split_prob = 0.01;
+  p->kappa_control = 2.0;
+  p->kappa_case = 2.0;
+}
+
+void hyg_tg_model_destroy(hyg_tg_model* m) {
+  if (!m) return;
+  if (m->on_device) {
+    (void)hipFree(m->d_consts);
+    (void)hipFree(m->d_hz);
+    (void)hipFree(m->d_lf);
+    (void)hipFree(m->d_lg);
+    (void)hipFree(m->d_cst);
+  }
+  delete m;
+}
+
+int hyg_tg_model_create(const hyg_tg_params* params, int32_t max_total_reads, int32_t max_duration,
+                        hyg_tg_model** out) {
+  if (!params || !out) return fail(HYG_EINVAL, "null argument");
+  *out = nullptr;
+  if (max_total_reads < 0 || max_total_reads > 65535) return fail(HYG_EINVAL, "max_total_reads out of [0, 65535]");
+  if (max_duration < 1 || max_duration >= HYG_DMAX - 2) return fail(HYG_EINVAL, "max_duration out of range");
+  auto* m = new hyg_tg_model();
+  int rc = hyg_tg_derive(params, &m->c);
+  if (rc != HYG_OK) {
+    delete m;
+    return fail(rc, "invalid model parameters");
+  }
+  m->max_duration = max_duration;
+  m->nmax_reads = max_total_reads;
+  m->dcap = hyg_hazard_len(&m->c, max_duration + 2);
+  const int K = m->c.K, L = max_total_reads + 1;
+  m->hz.resize((size_t)2 * K * m->dcap * 2);
+  hyg_hazard_fill(&m->c, m->dcap, m->hz.data());
+  m->lf.resize(L);
+  m->lg.resize((size_t)3 * K * L);
+  m->cst.resize(K);
+  hyg_bb_tables(&m->c, max_total_reads, m->lf.data(), m->lg.data(), m->cst.data());
+  if (have_device()) {
+    (void)hipGetDevice(&m->device);
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_consts, &m->c, 1);
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_hz, m->hz.data(), m->hz.size());
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_lf, m->lf.data(), m->lf.size());
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_lg, m->lg.data(), m->lg.size());
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_cst, m->cst.data(), m->cst.size());
+    m->on_device = true;
+    if (e != hipSuccess) {
+      hyg_tg_model_destroy(m);
+      return fail(HYG_EDEVICE, std::string("device upload failed: ") + hipGetErrorString(e));
+    }
+  }
+  *out = m;
+  return HYG_OK;
+}
+
+int32_t hyg_tg_num_particles(const hyg_tg_model* m) { return m ? m->c.Nmax : 0; }
+
+int hyg_tg_emission(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_t* tot_c, int32_t s_c,
+                    const uint16_t* meth_k, const uint16_t* tot_k, int32_t s_k, int64_t n_sites, double* E,
+                    void* stream) {
+  if (!m) return fail(HYG_EINVAL, "null model");
+  if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (s_c < 0 || s_k < 0 || n_sites < 0) return fail(HYG_EINVAL, "negative size");
+  if (n_sites > 0 && (!E || (s_c && (!meth_c || !tot_c)) || (s_k && (!meth_k || !tot_k))))
+    return fail(HYG_EINVAL, "null buffer");
+  return launch_emission(m->dev(), m->c, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E, stream);
+}
+
+static size_t header_bytes(int32_t n_chains) {
+  const size_t h = sizeof(ChainDev) * (size_t)n_chains + (sizeof(int32_t) + sizeof(double)) * (size_t)n_chains;
+  return (h + 255) / 256 * 256;
+}
+
+size_t hyg_tg_workspace_bytes(const hyg_tg_model* m, int32_t n_chains, int64_t total_steps) {
+  if (!m || n_chains < 0 || total_steps < 0) return 0;
+  return header_bytes(n_chains) + (size_t)total_steps * record_bytes(m->c.M) + 256;
+}
+
+int hyg_tg_run_chains(const hyg_tg_model* m, const hyg_tg_chain* chains, int32_t n_chains, const double* E,
+                      void* workspace, size_t workspace_bytes, const hyg_tg_outputs* out, void* stream) {
+  if (!m || !chains || !out || !E || !workspace) return fail(HYG_EINVAL, "null argument");
+  if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (n_chains <= 0) return HYG_OK;
+  if (!out->merged || !out->control || !out->kase || !out->split_probs || !out->regime_probs || !out->log_z)
+    return fail(HYG_EINVAL, "null output buffer");
+  if (!m->c.optimal) return fail(HYG_EUNSUPPORTED, "optimal_resampling = 0 is not implemented on the GPU path");
+  std::vector<ChainDev> cd(n_chains);
+  const size_t hb = header_bytes(n_chains);
+  size_t off = hb;
+  const size_t rb = record_bytes(m->c.M);
+  for (int i = 0; i < n_chains; ++i) {
+    const hyg_tg_chain& c = chains[i];
+    if (c.n_sites < 1) return fail(HYG_EINVAL, "chain with no sites");
+    if (c.n_sites > m->max_duration) return fail(HYG_EINVAL, "chain longer than the model's max_duration");
+    if (c.site_begin < 0 || c.out_begin < 0) return fail(HYG_EINVAL, "negative chain offset");
+    cd[i].site_begin = c.site_begin;
+    cd[i].out_begin = c.out_begin;
+    cd[i].ws_offset = (int64_t)off;
+    cd[i].seed = c.seed;
+    cd[i].chain_id = c.chain_id;
+    cd[i].T = c.n_sites;
+    cd[i].pad = 0;
+    off += (size_t)c.n_sites * rb;
+  }
+  if (off > workspace_bytes) return fail(HYG_EINVAL, "workspace too small (see hyg_tg_workspace_bytes)");
+  uint8_t* ws = (uint8_t*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(ws, cd.data(), sizeof(ChainDev) * n_chains, hipMemcpyHostToDevice, s) != hipSuccess)
+    return fail(HYG_EDEVICE, "descriptor upload failed");
+  hyg_tg_outputs o = *out;
+  if (!o.status) o.status = (int32_t*)(ws + sizeof(ChainDev) * n_chains);
+  int rc = launch_chains(m->dev(), m->c, (const ChainDev*)ws, n_chains, E, ws, o, stream);
+  if (rc == HYG_EUNSUPPORTED) return fail(rc, "particle arrays exceed the 160 KiB LDS of a CU (K too large)");
+  if (rc != HYG_OK) return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  return HYG_OK;
+}
+
+int hyg_tg_run_chain_host(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_t* tot_c, int32_t s_c,
+                          const uint16_t* meth_k, const uint16_t* tot_k, int32_t s_k, int32_t T, uint64_t seed,
+                          uint64_t chain_id, int16_t* merged, int16_t* control, int16_t* kase, float* split,
+                          float* regime, double* log_z, double* final_w) {
+  if (!m) return fail(HYG_EINVAL, "null model");
+  if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (T < 1) return fail(HYG_EINVAL, "no sites");
+  for (int64_t i = 0; i < (int64_t)T * s_c; ++i)
+    if (meth_c[i] > tot_c[i] || tot_c[i] > m->nmax_reads) return fail(HYG_EINVAL, "invalid control counts");
+  for (int64_t i = 0; i < (int64_t)T * s_k; ++i)
+    if (meth_k[i] > tot_k[i] || tot_k[i] > m->nmax_reads) return fail(HYG_EINVAL, "invalid case counts");
+  const int K = m->c.K, B = m->c.B, Nmax = m->c.Nmax;
+  struct Buf {
+    void* p = nullptr;
+    ~Buf() { if (p) (void)hipFree(p); }
+  } b_mc, b_tc, b_mk, b_tk, b_E, b_ws, b_mg, b_ct, b_ks, b_sp, b_rp, b_lz, b_fw, b_st;
+  auto alloc = [](Buf& b, size_t n) { return hipMalloc(&b.p, n ? n : 1) == hipSuccess; };
+  const size_t nc = (size_t)T * s_c, nk = (size_t)T * s_k;
+  const size_t wsb = hyg_tg_workspace_bytes(m, 1, T);
+  bool ok = alloc(b_mc, nc * 2) && alloc(b_tc, nc * 2) && alloc(b_mk, nk * 2) && alloc(b_tk, nk * 2) &&
+            alloc(b_E, sizeof(double) * T * 2 * K) && alloc(b_ws, wsb) && alloc(b_mg, 2 * (size_t)T * B) &&
+            alloc(b_ct, 4 * (size_t)T * B) && alloc(b_ks, 4 * (size_t)T * B) && alloc(b_sp, 4 * (size_t)T) &&
+            alloc(b_rp, 4 * (size_t)T * 2 * K) && alloc(b_lz, 8) && alloc(b_fw, 8 * (size_t)Nmax) && alloc(b_st, 4);
+  if (!ok) return fail(HYG_ENOMEM, "device allocation failed");
+  if (hipMemcpy(b_mc.p, meth_c, nc * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(b_tc.p, tot_c, nc * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(b_mk.p, meth_k, nk * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(b_tk.p, tot_k, nk * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  int rc = hyg_tg_emission(m, (uint16_t*)b_mc.p, (uint16_t*)b_tc.p, s_c, (uint16_t*)b_mk.p, (uint16_t*)b_tk.p, s_k, T,
+                           (double*)b_E.p, nullptr);
+  if (rc) return rc;
+  hyg_tg_chain ch{};
+  ch.site_begin = 0;
+  ch.n_sites = T;
+  ch.seed = seed;
+  ch.chain_id = chain_id;
+  ch.out_begin = 0;
+  hyg_tg_outputs o{};
+  o.merged = (int16_t*)b_mg.p;
+  o.control = (int16_t*)b_ct.p;
+  o.kase = (int16_t*)b_ks.p;
+  o.split_probs = (float*)b_sp.p;
+  o.regime_probs = (float*)b_rp.p;
+  o.log_z = (double*)b_lz.p;
+  o.final_log_weights = (double*)b_fw.p;
+  o.status = (int32_t*)b_st.p;
+  rc = hyg_tg_run_chains(m, &ch, 1, (double*)b_E.p, b_ws.p, wsb, &o, nullptr);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(HYG_EDEVICE, "kernel execution failed");
+  int32_t st = 0;
+  if (hipMemcpy(&st, b_st.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(merged, b_mg.p, 2 * (size_t)T * B, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(control, b_ct.p, 4 * (size_t)T * B, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(kase, b_ks.p, 4 * (size_t)T * B, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(split, b_sp.p, 4 * (size_t)T, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(regime, b_rp.p, 4 * (size_t)T * 2 * K, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(log_z, b_lz.p, 8, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (final_w && hipMemcpy(final_w, b_fw.p, 8 * (size_t)Nmax, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (st != HYG_OK) return fail(st, "all particle weights became -inf");
+  return HYG_OK;
+}
+
+void hyg_set_kernel_timing(int enable) { set_kernel_timing(enable != 0); }
+
+int hyg_tg_last_kernel_ms(float* ms3) {
+  if (!ms3) return fail(HYG_EINVAL, "null argument");
+  return last_kernel_ms(ms3);
+}
+
+}  // extern "C"

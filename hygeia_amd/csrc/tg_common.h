@@ -1,0 +1,69 @@
+// Internal types shared by the host library (capi.cpp) and the kernels
+// (tg_kernels.hip). Not part of the public ABI.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/hyg_model.h"
+
+namespace hyg {
+
+constexpr int kThreads = 256;  // one workgroup (4 waves) per chain
+constexpr int kEBlock = 32;    // emission rows staged in LDS per block of steps
+
+// Device-side chain descriptor (lives in the workspace header).
+struct ChainDev {
+  int64_t site_begin;
+  int64_t out_begin;
+  int64_t ws_offset;  // byte offset of the chain's history records
+  uint64_t seed;
+  uint64_t chain_id;
+  int32_t T;
+  int32_t pad;
+};
+
+// Per-step history record: scalars, then M packed parent states, then M
+// parent weights. Written by the forward kernel, read by the backward kernel.
+struct StepScalars {
+  int32_t mode;   // 0 keep, 1 optimal, 2 unbiased, 3 init
+  int32_t n_par;
+  float log_c;
+  int32_t r_ph;
+  double lse;
+  double pad;
+};
+static_assert(sizeof(StepScalars) == 32, "record scalars");
+
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline size_t record_bytes(int M) { return sizeof(StepScalars) + (size_t)M * 16; }
+
+struct ModelDev {
+  const hyg_tg_consts* consts;  // device copy
+  const double* hz;             // [2][K][dcap][2]
+  int32_t dcap;
+  int32_t nmax_reads;
+  const double* lf;   // [nmax+1]
+  const double* lg;   // [K][3][nmax+1]
+  const double* cst;  // [K]
+};
+
+struct FwdLayout {  // LDS carve of the forward kernel (byte offsets)
+  size_t W, keys, mass, pst, pw, phz, ering, cp, misc, total;
+  int npad, nsort;
+};
+
+// Launchers (tg_kernels.hip)
+int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* meth_c, const uint16_t* tot_c,
+                    int s_c, const uint16_t* meth_k, const uint16_t* tot_k, int s_k, int64_t n_sites,
+                    double* E, void* stream);
+int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
+                  const double* E, uint8_t* ws, const hyg_tg_outputs& out, void* stream);
+size_t forward_lds_bytes(const hyg_tg_consts& c);
+void set_kernel_timing(bool on);
+int last_kernel_ms(float* out3);
+size_t backward_lds_bytes(const hyg_tg_consts& c);
+
+}  // namespace hyg

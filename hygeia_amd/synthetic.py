@@ -118,3 +118,45 @@ def segment_chains(chrom_sizes, segment_size: int = 100000, buffer_size: int = 5
             chains.append((ci, b, base + lo, hi - lo, r0, max(0, r1 - r0)))
         base += n
     return chains
+
+
+def simulate_device(n_sites: int, n_ctrl: int, n_case: int, K: int = 6, u: int = 3, omega: float = 0.8,
+                    kappa: float = 2.0, coverage: float = 100.0, split_frac: float = 0.1, seed: int = DATA_SEED,
+                    device=None):
+    """simulate() with the per-sample draws (Beta levels, Poisson coverage,
+    Binomial counts) done on the GPU with torch: 28M sites in seconds. Returns
+    int16 device tensors holding the uint16 count bit patterns [T][S]."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    mu, sigma = regime_params(K)
+    nu = mu * (1 - mu) / sigma ** 2 - 1
+    alpha, beta = torch.tensor(mu * nu, device=device), torch.tensor((1 - mu) * nu, device=device)
+    r_ctrl = _segments(rng, n_sites, K, u, kappa, omega).astype(np.int8)
+    mean_split = 200.0
+    n_str = max(1, int(n_sites * split_frac / mean_split))
+    starts = rng.integers(0, n_sites, size=n_str)
+    lens = rng.geometric(1.0 / mean_split, size=n_str)
+    delta = np.zeros(n_sites + 1, dtype=np.int32)
+    np.add.at(delta, starts, 1)
+    np.add.at(delta, np.minimum(starts + lens, n_sites), -1)
+    split = np.cumsum(delta[:-1]) > 0
+    r_case = np.where(split, _segments(rng, n_sites, K, u, kappa, omega).astype(np.int8), r_ctrl)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    torch.manual_seed(seed)
+    out = {}
+    for name, reg, S in (("control", r_ctrl, n_ctrl), ("case", r_case, n_case)):
+        rg = torch.from_numpy(reg.astype(np.int64)).to(device)
+        a = alpha[rg][:, None].expand(n_sites, S).float()
+        b = beta[rg][:, None].expand(n_sites, S).float()
+        lvl = torch.distributions.Beta(a, b).sample()
+        tot = torch.poisson(torch.full((n_sites, S), float(coverage), device=device), generator=gen)
+        tot = tot.clamp(max=65535.0)
+        meth = torch.binomial(tot, lvl.clamp(0.0, 1.0), generator=gen)
+        out[f"tot_{name}"] = tot.to(torch.int32).to(torch.int16).contiguous()
+        out[f"meth_{name}"] = meth.to(torch.int32).to(torch.int16).contiguous()
+        del a, b, lvl, tot, meth
+    out["regime_control"] = r_ctrl
+    out["regime_case"] = r_case
+    return out

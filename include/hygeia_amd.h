@@ -146,6 +146,13 @@ int hyg_tg_run_chain_host(const hyg_tg_model* model, const uint16_t* meth_ctrl, 
                           int16_t* kase, float* split_probs, float* regime_probs, double* log_z,
                           double* final_log_weights);
 
+/* Kernel timing for benchmarks: when enabled, HIP events are recorded on the
+ * launch stream around the emission, forward and backward kernels;
+ * hyg_tg_last_kernel_ms waits for the last ones and returns their durations
+ * in ms (-1 for a kernel not launched since timing was enabled). */
+void hyg_set_kernel_timing(int enable);
+int hyg_tg_last_kernel_ms(float* ms3);
+
 /* Number of visible HIP devices (0 when none: compute calls then fail). */
 int hyg_device_count(void);
 const char* hyg_last_error(void);

@@ -1,0 +1,171 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact trajectories (merged / control / case int16 arrays), bit-exact
+split and regime probabilities (f32), bit-exact log normalising constant and
+final weights (f64) -- the arithmetic contract of include/hyg_arith.h makes the
+kernels and the oracle compute the same numbers.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _have_gpu():
+    from hygeia_amd import _lib
+
+    return _lib.load().hyg_device_count() > 0
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not _have_gpu():
+        pytest.fail("no HIP device visible: the GPU tests must run on an MI355X (gpurun)")
+
+
+def _setup(oracle, K, M, B, T, S, cov, dseed, split_frac=0.1):
+    from hygeia_amd import synthetic as syn
+
+    mu, sg = syn.regime_params(K)
+    d = syn.simulate(T, S, S, K=K, seed=dseed, coverage=cov, split_frac=split_frac)
+    p = oracle.make_params(K=K, M=M, B=B, mu=mu, sigma=sg)
+    theta = np.array(p.theta[: p.theta_len])
+    return mu, sg, theta, d, p
+
+
+def _model(mu, sg, theta, M, B, max_reads, max_dur):
+    from hygeia_amd import two_group
+
+    return two_group.CaseControlModel(mu, sg, theta, num_resampled_ancestors=M, num_samples_backward=B,
+                                      max_total_reads=max_reads, max_duration=max_dur)
+
+
+CASES = [
+    # K, M, B, T, S, coverage, data seed, inference seed
+    (6, 50, 25, 1500, 4, 100.0, 11, 0),   # the pipeline configuration, short chain
+    (6, 50, 25, 800, 4, 1000.0, 12, 1),   # high coverage: unbiased-fallback steps occur
+    (6, 10, 5, 600, 2, 30.0, 13, 2),      # small M / B
+    (4, 20, 8, 700, 3, 60.0, 14, 3),
+    (3, 7, 4, 500, 1, 10.0, 15, 4),       # K = 3, one sample per group
+    (2, 5, 3, 300, 2, 20.0, 16, 5),       # K = 2 (empty uniform case-regime sets)
+    (6, 50, 25, 1, 4, 100.0, 17, 6),      # a single site: no filter step
+    (6, 50, 25, 2, 4, 100.0, 18, 7),
+    (6, 50, 25, 5, 4, 100.0, 19, 8),
+]
+
+
+@pytest.mark.parametrize("K,M,B,T,S,cov,dseed,seed", CASES)
+def test_chain_bit_exact(oracle, K, M, B, T, S, cov, dseed, seed):
+    from hygeia_amd import two_group
+
+    mu, sg, theta, d, p = _setup(oracle, K, M, B, T, S, cov, dseed)
+    E = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    ref = oracle.chain(p, E, seed, 1000 + seed)
+    assert ref["status"] == 0
+    maxr = int(max(d["tot_control"].max(), d["tot_case"].max()))
+    model = _model(mu, sg, theta, M, B, maxr, T + 5)
+    res, fw, ex = two_group.run({"control": d["meth_control"], "case": d["meth_case"]},
+                                {"control": d["tot_control"], "case": d["tot_case"]}, model, seed, 1000 + seed)
+    pr = res.particle
+    np.testing.assert_array_equal(pr["merged_state"], ref["merged"])
+    np.testing.assert_array_equal(pr["control_state"], ref["control"])
+    np.testing.assert_array_equal(pr["case_state"], ref["case"])
+    np.testing.assert_array_equal(ex["split_probs"], ref["split_probs"])
+    np.testing.assert_array_equal(ex["regime_probs"], ref["regime_probs"])
+    assert ex["log_z"] == ref["log_z"]
+    np.testing.assert_array_equal(fw, ref["final_log_weights"])
+
+
+def test_zero_coverage_stretch(oracle):
+    """Missing data (n = 0 for every sample) contributes exactly 0 (TFP BB at n=0)."""
+    from hygeia_amd import two_group
+
+    mu, sg, theta, d, p = _setup(oracle, 6, 50, 25, 900, 4, 80.0, 21)
+    for k in ("meth_control", "tot_control", "meth_case", "tot_case"):
+        d[k][200:400] = 0
+        d[k][600:610, :2] = 0
+    E = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    assert np.all(E[200:400] == 0.0)
+    ref = oracle.chain(p, E, 3, 77)
+    model = _model(mu, sg, theta, 50, 25, int(d["tot_case"].max()), 1000)
+    res, fw, ex = two_group.run({"control": d["meth_control"], "case": d["meth_case"]},
+                                {"control": d["tot_control"], "case": d["tot_case"]}, model, 3, 77)
+    np.testing.assert_array_equal(res.particle["control_state"], ref["control"])
+    np.testing.assert_array_equal(res.particle["case_state"], ref["case"])
+    np.testing.assert_array_equal(ex["regime_probs"], ref["regime_probs"])
+
+
+def test_batched_chains_and_emission(oracle):
+    """Many chains of different lengths in one launch (the sharded driver's
+    path), device-resident inputs; each chain equals its own oracle run."""
+    from hygeia_amd import two_group
+
+    K, M, B, S = 6, 50, 25, 4
+    mu, sg, theta, d, p = _setup(oracle, K, M, B, 5300, S, 100.0, 31)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(d[k]).view(np.int16)).to(dev) for k in
+         ("meth_control", "tot_control", "meth_case", "tot_case")}
+    lengths = [1000, 37, 1, 2200, 963, 1000]
+    chains, site, out = [], 0, 0
+    for i, n in enumerate(lengths):
+        chains.append((site, n, 5 + i % 2, 900 + i, out))
+        site += n
+        out += n
+    model = _model(mu, sg, theta, M, B, int(max(d["tot_control"].max(), d["tot_case"].max())), 3000)
+    dc = two_group.DeviceChains(model, chains, out, device=dev, final_weights=True)
+    E = dc.emission(t["meth_control"], t["tot_control"], t["meth_case"], t["tot_case"])
+    dc.run(E)
+    torch.cuda.synchronize()
+    E_ref = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    np.testing.assert_array_equal(E.cpu().numpy(), E_ref)
+    assert (dc.status.cpu().numpy() == 0).all()
+    for i, (s0, n, seed, cid, o0) in enumerate(chains):
+        ref = oracle.chain(p, E_ref[s0:s0 + n], seed, cid)
+        np.testing.assert_array_equal(dc.merged[o0:o0 + n].cpu().numpy(), ref["merged"])
+        np.testing.assert_array_equal(dc.control[o0:o0 + n].cpu().numpy(), ref["control"])
+        np.testing.assert_array_equal(dc.case[o0:o0 + n].cpu().numpy(), ref["case"])
+        np.testing.assert_array_equal(dc.split_probs[o0:o0 + n].cpu().numpy(), ref["split_probs"])
+        np.testing.assert_array_equal(dc.regime_probs[o0:o0 + n].cpu().numpy(), ref["regime_probs"])
+        assert dc.log_z[i].item() == ref["log_z"]
+        np.testing.assert_array_equal(dc.final_w[i].cpu().numpy(), ref["final_log_weights"])
+
+
+def test_long_chain_properties_and_determinism():
+    """A full-length segment chain (110k sites, the reference's segment +
+    buffers): size-independent properties, and bit-identical reruns."""
+    from hygeia_amd import synthetic as syn
+    from hygeia_amd import two_group
+
+    T = 110000
+    d = syn.simulate(T, 4, 4, K=6, seed=41, coverage=100.0)
+    mu, sg = syn.regime_params(6)
+    theta = two_group.uniform_theta(6)
+    model = _model(mu, sg, theta, 50, 25, int(max(d["tot_control"].max(), d["tot_case"].max())), T)
+    obs = {"control": d["meth_control"], "case": d["meth_case"]}
+    tot = {"control": d["tot_control"], "case": d["tot_case"]}
+    res, fw, ex = two_group.run(obs, tot, model, 0, 1)
+    res2, fw2, ex2 = two_group.run(obs, tot, model, 0, 1)
+    ctl = res.particle["control_state"].astype(np.int64)
+    case = res.particle["case_state"].astype(np.int64)
+    m = res.particle["merged_state"]
+    np.testing.assert_array_equal(ctl, res2.particle["control_state"])
+    np.testing.assert_array_equal(ex["regime_probs"], ex2["regime_probs"])
+    # durations advance by one or restart at a change point (int16 wrap aside)
+    dd = (ctl[1:, :, 0] - ctl[:-1, :, 0]) % 65536
+    assert np.all((dd == 1) | (ctl[1:, :, 0] == 1))
+    # regimes only change at change points
+    assert np.all((ctl[1:, :, 1] == ctl[:-1, :, 1]) | (ctl[1:, :, 0] == 1))
+    # merged sites carry identical control and case states
+    mm = m == 1
+    assert np.all(ctl[mm] == case[mm])
+    # probabilities are means over B: regime probs of each group sum to 1
+    rp = ex["regime_probs"]
+    np.testing.assert_allclose(rp[:, :6].sum(1), 1.0, atol=1e-6)
+    np.testing.assert_allclose(rp[:, 6:].sum(1), 1.0, atol=1e-6)
+    np.testing.assert_array_equal(ex["split_probs"], (m == 0).mean(1).astype(np.float32))
+    # recovery of the simulated control regimes
+    acc = (rp[:, :6].argmax(1) == d["regime_control"]).mean()
+    assert acc > 0.95, acc
+    assert np.isfinite(ex["log_z"])
