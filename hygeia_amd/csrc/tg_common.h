@@ -9,8 +9,8 @@
 
 namespace hyg {
 
-constexpr int kThreads = 256;  // one workgroup (4 waves) per chain
-constexpr int kEBlock = 32;    // emission rows staged in LDS per block of steps
+constexpr int kDefaultThreads = 256;  // threads of the per-chain workgroup (HYG_THREADS overrides)
+constexpr int kEBlock = 16;    // emission rows staged in LDS per block of steps
 
 // Device-side chain descriptor (lives in the workspace header).
 struct ChainDev {

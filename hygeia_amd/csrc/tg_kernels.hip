@@ -1,18 +1,28 @@
 // tg_kernels.hip -- CDNA4 (gfx950) kernels of the two-group change-point path.
 //
-//   tg_emission_kernel  per-site Beta-Binomial emission table (HBM streaming)
-//   tg_forward_kernel   particle filter with optimal finite-state resampling,
-//                       one 256-thread workgroup per chain, persistent over T
-//   tg_backward_kernel  backward simulation of B trajectories, one workgroup
-//                       per chain, regenerating each step's particles from the
-//                       forward's ancestor history
+//   tg_emission_kernel   per-site Beta-Binomial emission table (HBM streaming)
+//   tg_forward_kernel    particle filter with optimal finite-state resampling,
+//                        one workgroup per chain, persistent over the T sites
+//   tg_backward_kernel   backward simulation of B trajectories, one workgroup
+//                        per chain, regenerating each step's particles from the
+//                        forward's ancestor history (read one step ahead)
 //
 // Every index decision uses the arithmetic contract of include/hyg_arith.h
 // (exact integer mass sums, deterministic exp/log, Philox streams), so the
-// results are bit-identical to the CPU oracle (oracle/tg_oracle.c) whatever
-// the reduction tree; that freedom is what the kernels use to parallelise.
-// Reference semantics: see the oracle header and DESIGN.md.
+// results are bit-identical to the CPU oracle (oracle/tg_oracle.c) whatever the
+// reduction tree; that freedom is what the kernels use to parallelise.
+//
+// Latency design (one chain = a sequential recursion of ~110k steps, so the
+// per-step critical path is what matters): model constants and hazard rows
+// are read from LDS (hazard rows of the next step's ancestors are prefetched
+// one step ahead), the resampling sort runs in registers / wave shuffles with
+// LDS only for cross-wave stages, the K / log c search runs in one wave with
+// 64-way probes, and reductions are fused to two block barriers per step.
 #include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "../../include/hyg_arith.h"
 #include "tg_common.h"
@@ -28,11 +38,10 @@ __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ unsigned long long shx(unsigned long long v, int o) { return __shfl_xor(v, o); }
 __device__ __forceinline__ unsigned long long shu(unsigned long long v, int o) { return __shfl_up(v, o); }
 
+__device__ __forceinline__ double dmax(double a, double b) { return (b > a) ? b : a; }
+
 __device__ __forceinline__ double wave_max(double v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const double w = __shfl_xor(v, o);
-    v = (w > v) ? w : v;
-  }
+  for (int o = 32; o > 0; o >>= 1) v = dmax(v, __shfl_xor(v, o));
   return v;
 }
 __device__ __forceinline__ int wave_sum(int v) {
@@ -49,28 +58,38 @@ __device__ __forceinline__ hyg_u128 wave_sum128(hyg_u128 v) {
   return v;
 }
 
-// Block-wide reductions (4 waves). `red` is a 128-byte LDS scratch; every call
-// begins with a barrier so back-to-back calls may reuse it.
+// Block-wide reductions. `red` is an LDS scratch of at least 32 B per wave;
+// every call starts with a barrier so consecutive calls may reuse it.
+template <int NT>
+__device__ __forceinline__ void block_max_cnt(double m, int c, unsigned char* red, double* m_out, int* c_out) {
+  m = wave_max(m);
+  c = wave_sum(c);
+  __syncthreads();
+  if (lane_id() == 0) {
+    ((double*)red)[2 * wave_id()] = m;
+    ((int*)red)[4 * wave_id() + 2] = c;
+  }
+  __syncthreads();
+  double mm = ((double*)red)[0];
+  int cc = ((int*)red)[2];
+  for (int w = 1; w < NT / 64; ++w) {
+    mm = dmax(mm, ((double*)red)[2 * w]);
+    cc += ((int*)red)[4 * w + 2];
+  }
+  *m_out = mm;
+  *c_out = cc;
+}
+template <int NT>
 __device__ __forceinline__ double block_max(double v, unsigned char* red) {
-  double* r = (double*)red;
   v = wave_max(v);
   __syncthreads();
-  if (lane_id() == 0) r[wave_id()] = v;
+  if (lane_id() == 0) ((double*)red)[wave_id()] = v;
   __syncthreads();
-  double m = r[0];
-  for (int w = 1; w < kThreads / 64; ++w) m = (r[w] > m) ? r[w] : m;
+  double m = ((double*)red)[0];
+  for (int w = 1; w < NT / 64; ++w) m = dmax(m, ((double*)red)[w]);
   return m;
 }
-__device__ __forceinline__ int block_sum(int v, unsigned char* red) {
-  int* r = (int*)red;
-  v = wave_sum(v);
-  __syncthreads();
-  if (lane_id() == 0) r[wave_id()] = v;
-  __syncthreads();
-  int s = 0;
-  for (int w = 0; w < kThreads / 64; ++w) s += r[w];
-  return s;
-}
+template <int NT>
 __device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red) {
   hyg_u128* r = (hyg_u128*)red;
   v = wave_sum128(v);
@@ -78,12 +97,15 @@ __device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red)
   if (lane_id() == 0) r[wave_id()] = v;
   __syncthreads();
   hyg_u128 s = hyg_u128_zero();
-  for (int w = 0; w < kThreads / 64; ++w) s = hyg_u128_add(s, r[w]);
+  for (int w = 0; w < NT / 64; ++w) s = hyg_u128_add(s, r[w]);
   return s;
 }
 
-// Exclusive block scans; out[tid] = exclusive prefix, out[kThreads] = total.
-__device__ __forceinline__ void block_scan192(hyg_u192 v, hyg_u192* out, unsigned char* red) {
+// Exclusive block scans. The register forms return this thread's exclusive
+// prefix and the block total; the array form writes out[tid] (exclusive) and
+// out[NT] (total) for searches.
+template <int NT>
+__device__ __forceinline__ hyg_u192 block_excl192(hyg_u192 v, unsigned char* red, hyg_u192* total) {
   hyg_u192* r = (hyg_u192*)red;
   hyg_u192 inc = v;
   for (int o = 1; o < 64; o <<= 1) {
@@ -97,13 +119,33 @@ __device__ __forceinline__ void block_scan192(hyg_u192 v, hyg_u192* out, unsigne
   if (lane_id() == 63) r[wave_id()] = inc;
   __syncthreads();
   hyg_u192 pre = hyg_u192_zero(), tot = hyg_u192_zero();
-  for (int w = 0; w < kThreads / 64; ++w) {
+  for (int w = 0; w < NT / 64; ++w) {
     if (w < wave_id()) pre = hyg_u192_add(pre, r[w]);
     tot = hyg_u192_add(tot, r[w]);
   }
-  out[threadIdx.x] = hyg_u192_add(pre, hyg_u192_sub(inc, v));
-  if (threadIdx.x == 0) out[kThreads] = tot;
+  *total = tot;
+  return hyg_u192_add(pre, hyg_u192_sub(inc, v));
 }
+template <int NT>
+__device__ __forceinline__ int block_excl_int(int v, unsigned char* red, int* total) {
+  int* r = (int*)red;
+  int inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int n = __shfl_up(inc, o);
+    if (lane_id() >= o) inc += n;
+  }
+  __syncthreads();
+  if (lane_id() == 63) r[wave_id()] = inc;
+  __syncthreads();
+  int pre = 0, tot = 0;
+  for (int w = 0; w < NT / 64; ++w) {
+    if (w < wave_id()) pre += r[w];
+    tot += r[w];
+  }
+  *total = tot;
+  return pre + inc - v;
+}
+template <int NT>
 __device__ __forceinline__ void block_scan128(hyg_u128 v, hyg_u128* out, unsigned char* red) {
   hyg_u128* r = (hyg_u128*)red;
   hyg_u128 inc = v;
@@ -117,20 +159,15 @@ __device__ __forceinline__ void block_scan128(hyg_u128 v, hyg_u128* out, unsigne
   if (lane_id() == 63) r[wave_id()] = inc;
   __syncthreads();
   hyg_u128 pre = hyg_u128_zero(), tot = hyg_u128_zero();
-  for (int w = 0; w < kThreads / 64; ++w) {
+  for (int w = 0; w < NT / 64; ++w) {
     if (w < wave_id()) pre = hyg_u128_add(pre, r[w]);
     tot = hyg_u128_add(tot, r[w]);
   }
-  // exclusive = inclusive - v, computed without a 128-bit subtract
-  hyg_u128 ex = pre;
-  {
-    hyg_u128 e2;  // inc - v
-    e2.lo = inc.lo - v.lo;
-    e2.hi = inc.hi - v.hi - (inc.lo < v.lo ? 1u : 0u);
-    ex = hyg_u128_add(ex, e2);
-  }
-  out[threadIdx.x] = ex;
-  if (threadIdx.x == 0) out[kThreads] = tot;
+  hyg_u128 e2;  // inc - v
+  e2.lo = inc.lo - v.lo;
+  e2.hi = inc.hi - v.hi - (inc.lo < v.lo ? 1u : 0u);
+  out[threadIdx.x] = hyg_u128_add(pre, e2);
+  if (threadIdx.x == 0) out[NT] = tot;
 }
 
 // sort key: ascending key == descending f32 value, ties by ascending index
@@ -147,48 +184,75 @@ __device__ __forceinline__ float key_value(uint64_t k) {
 }
 __device__ __forceinline__ int key_index(uint64_t k) { return (int)(uint32_t)k; }
 
+// n / d for 0 <= n < 2^22, 1 <= d <= 2^22, via a float reciprocal + fixup
+__device__ __forceinline__ int fdiv(int n, int d, float rd) {
+  int q = (int)((float)n * rd);
+  if (q * d > n) --q;
+  if ((q + 1) * d <= n) ++q;
+  return q;
+}
+
 // --------------------------------------------------------------- model
 struct Hz4 {
-  double lrc, l1c, lrk, l1k;  // log rho / log(1-rho), control (d_c, r_c) and case (d_k, r_k)
+  double lrc, l1c, lrk, l1k;  // log rho / log(1-rho) of control (d_c, r_c) and case (d_k, r_k)
+};
+
+struct ConstLds {  // model constants staged in LDS
+  double lPc[HYG_KMAX * HYG_KMAX];
+  double lPm[4];
+  double lU1, lU2, log_M;
+  double2 hz1[2][HYG_KMAX];  // hazard rows at d = 1
+  float logMa[64];           // (float)log(M - a) for a < min(M, 64) (resampling_functions.py:13)
+  int u, K;
 };
 
 __device__ __forceinline__ double2 hz_at(const ModelDev& md, int K, int g, int r, int d) {
   d = d < 0 ? 0 : (d >= md.dcap ? md.dcap - 1 : d);
   return *(const double2*)(md.hz + ((size_t)(g * K + r) * md.dcap + d) * 2);
 }
-__device__ __forceinline__ Hz4 hz_of(const ModelDev& md, int K, uint64_t s) {
-  const double2 a = hz_at(md, K, 0, hyg_st_rc(s), hyg_st_dc(s));
-  const double2 b = hz_at(md, K, 1, hyg_st_rk(s), hyg_st_dk(s));
-  Hz4 h;
-  h.lrc = a.x; h.l1c = a.y; h.lrk = b.x; h.l1k = b.y;
-  return h;
+
+__device__ __forceinline__ void load_consts(ConstLds& cl, const hyg_tg_consts* __restrict__ c, const ModelDev& md) {
+  const int K = c->K;
+  for (int i = threadIdx.x; i < K * K; i += blockDim.x) cl.lPc[i] = c->lPc[i];
+  if (threadIdx.x < 4) cl.lPm[threadIdx.x] = c->lPm[threadIdx.x];
+  if (threadIdx.x < 2 * K) {
+    const int g = threadIdx.x / K, r = threadIdx.x - g * K;
+    cl.hz1[g][r] = hz_at(md, K, g, r, 1);
+  }
+  if (threadIdx.x < 64 && threadIdx.x < c->M) cl.logMa[threadIdx.x] = hyg_logf((float)(c->M - (int)threadIdx.x));
+  if (threadIdx.x == 0) {
+    cl.lU1 = c->lU1;
+    cl.lU2 = c->lU2;
+    cl.log_M = c->log_M;
+    cl.u = c->u;
+    cl.K = K;
+  }
 }
 
 // log f_t(next | prev), t >= 1 (case_control_regime_model.py:80-193,
 // case_control_distributions.py:138-151, 246-291); h = hazard of prev.
 // Same branch structure and addition order as oracle/tg_oracle.c:tg_trans.
-__device__ __forceinline__ double tg_trans(const hyg_tg_consts* __restrict__ c, int K, uint64_t prev, uint64_t next,
-                                           const Hz4& h) {
+__device__ __forceinline__ double tg_trans(const ConstLds& cl, int K, uint64_t prev, uint64_t next, const Hz4& h) {
   const double NINF = HYG_NINF;
   const int m = hyg_st_m(prev), dc = hyg_st_dc(prev), rc = hyg_st_rc(prev), dk = hyg_st_dk(prev),
             rk = hyg_st_rk(prev);
   const int m2 = hyg_st_m(next), dc2 = hyg_st_dc(next), rc2 = hyg_st_rc(next), dk2 = hyg_st_dk(next),
             rk2 = hyg_st_rk(next);
   double lm;
-  if ((dk < dc ? dk : dc) >= c->u) lm = c->lPm[m * 2 + m2];
+  if ((dk < dc ? dk : dc) >= cl.u) lm = cl.lPm[m * 2 + m2];
   else lm = (m2 == m) ? 0.0 : NINF;
   double lc;
-  if (dc2 == 1) lc = h.lrc + c->lPc[rc * K + rc2];
+  if (dc2 == 1) lc = h.lrc + cl.lPc[rc * K + rc2];
   else lc = (dc2 == dc + 1 && rc2 == rc) ? h.l1c : NINF;
   double lk;
   if (m2 == 1) {
     lk = (rk2 == rc2 && dk2 == dc2) ? 0.0 : NINF;
   } else if (m == 1 && dc2 != 1) {
-    lk = (dk2 == 1 && rk2 != rc2) ? c->lU1 : NINF;
+    lk = (dk2 == 1 && rk2 != rc2) ? cl.lU1 : NINF;
   } else if (rc2 == rk && m == 0) {
-    lk = (dk2 == 1 && rk2 != rc2) ? c->lU1 : NINF;
+    lk = (dk2 == 1 && rk2 != rc2) ? cl.lU1 : NINF;
   } else {
-    if (dk2 == 1) lk = (rk2 != rc2 && rk2 != rk) ? h.lrk + ((rc2 == rk) ? c->lU1 : c->lU2) : NINF;
+    if (dk2 == 1) lk = (rk2 != rc2 && rk2 != rk) ? h.lrk + ((rc2 == rk) ? cl.lU1 : cl.lU2) : NINF;
     else lk = (dk2 == dk + 1 && rk2 == rk) ? h.l1k : NINF;
   }
   return (lm + lc) + lk;
@@ -219,14 +283,45 @@ __device__ __forceinline__ uint64_t init_state(int K, int n) {
   return hyg_st_pack(i == j, 1, i, 1, j);
 }
 
-// ----------------------------------------------------------- LDS layout
+// Hazard rows a child may need, prefetched per ancestor: control at
+// (d_c + 1, r_c), case at (d_k + 1, r_k), case at (d_c + 1, r_c) (merge slot).
+struct Pf3 {
+  double2 c1, k1, kc;
+};
+__device__ __forceinline__ Pf3 prefetch_rows(const ModelDev& md, int K, uint64_t a) {
+  Pf3 p;
+  const int dc = hyg_st_dc(a), rc = hyg_st_rc(a);
+  p.c1 = hz_at(md, K, 0, rc, dc + 1);
+  p.k1 = hz_at(md, K, 1, hyg_st_rk(a), hyg_st_dk(a) + 1);
+  p.kc = hz_at(md, K, 1, rc, dc + 1);
+  return p;
+}
+// Hazards of the child in slot s of ancestor a (the rows of the child's own
+// durations/regimes), from the ancestor's prefetched rows and the d = 1 rows.
+__device__ __forceinline__ Hz4 child_hz(const ConstLds& cl, int K, uint64_t a, int s, const Pf3& p,
+                                        const ModelDev& md) {
+  Hz4 h;
+  const uint64_t x = tg_xi(K, a, s);
+  double2 hc, hk;
+  if (s == 0) { hc = p.c1; hk = p.k1; }
+  else if (s < K) { hc = cl.hz1[0][hyg_st_rc(x)]; hk = p.k1; }
+  else if (s < 2 * K - 1) { hc = p.c1; hk = cl.hz1[1][hyg_st_rk(x)]; }
+  else if (s == 2 * K - 1) {
+    if (hyg_st_m(a) == 0) { hc = p.c1; hk = p.kc; }
+    else { hc = hz_at(md, K, 0, hyg_st_rc(x), 0); hk = hz_at(md, K, 1, hyg_st_rk(x), 0); }  // weight is -inf
+  } else { hc = cl.hz1[0][hyg_st_rc(x)]; hk = cl.hz1[1][hyg_st_rk(x)]; }
+  h.lrc = hc.x; h.l1c = hc.y; h.lrk = hk.x; h.l1k = hk.y;
+  return h;
+}
+
+// ------------------------------------------------------------ LDS layout
 struct Shared {  // broadcast scalars of one workgroup
-  double mx, logS, lse;
-  float c_new, log_c, U;
-  int cnt, n_sig, np, mode, Kk, status, r_ph;
+  double mx, logS;
+  float c_new, log_c;
+  int cnt, n_sig, Kk, status, r_ph, ng;
   unsigned sig_ctr;
-  hyg_u192 preK, R;
-  int ng;
+  hyg_u192 R, preK;
+  unsigned long long ph[24];
 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -236,144 +331,159 @@ __host__ __device__ inline int next_pow2(int x) {
   return p;
 }
 
+constexpr int kBuckets = 1024;  // counting-sort buckets of the resampling sort
+
 struct Lay {  // byte offsets into the dynamic LDS
-  size_t W, L, keys, mass, pst, pw, phz, ering, cp, parents, sysp, X, grp, gst, red, sh, total;
-  int npad, nsort;
+  size_t W, L, keys, bcnt, bpos, pre64, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, red, sh, total;
+  int npad, nkeys, nt;
 };
 
-__host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, bool backward) {
+__host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT, bool backward) {
   Lay l{};
-  l.npad = (int)align_up((size_t)Nmax, kThreads);
-  l.nsort = next_pow2(Nmax < 64 ? 64 : Nmax);
+  l.nt = NT;
+  l.npad = (int)align_up((size_t)Nmax, NT);
   size_t o = 0;
   l.W = o; o = align_up(o + sizeof(double) * l.npad, 16);
-  if (backward) { l.L = o; o = align_up(o + sizeof(double) * l.npad, 16); }
-  if (!backward) {
-    l.keys = o; o = align_up(o + sizeof(uint64_t) * l.nsort, 16);
-    l.mass = o; o = align_up(o + sizeof(float) * l.npad, 16);
+  if (backward) {
+    l.L = o; o = align_up(o + sizeof(double) * l.npad, 16);
+    l.cp = o; o = align_up(o + sizeof(hyg_u128) * (NT + 1), 16);
+  } else {
+    // sort keys; the unbiased fallback reuses them as its (NT+1) x u128 prefix array
+    size_t kb = sizeof(uint64_t) * (size_t)Nmax;
+    if (kb < sizeof(hyg_u128) * (size_t)(NT + 1)) kb = sizeof(hyg_u128) * (size_t)(NT + 1);
+    l.nkeys = (int)(kb / sizeof(uint64_t));
+    l.keys = o; o = align_up(o + kb, 16);
+    // bucket counts / positions; the systematic thresholds (M x u192) reuse them
+    size_t bb = sizeof(int) * 2 * kBuckets;
+    if (bb < sizeof(hyg_u192) * (size_t)M) bb = sizeof(hyg_u192) * (size_t)M;
+    l.bcnt = o;
+    l.bpos = o + sizeof(int) * kBuckets;
+    o = align_up(o + bb, 16);
+    l.pre64 = o; o = align_up(o + sizeof(hyg_u192) * 64, 16);
   }
   l.pst = o; o = align_up(o + sizeof(uint64_t) * 2 * M, 16);
   l.pw = o; o = align_up(o + sizeof(double) * 2 * M, 16);
-  l.phz = o; o = align_up(o + sizeof(double) * 4 * M, 16);
-  l.ering = o; o = align_up(o + sizeof(double) * kEBlock * 2 * K, 16);
-  l.cp = o; o = align_up(o + sizeof(hyg_u192) * (kThreads + 1), 16);
+  l.phz = o; o = align_up(o + sizeof(Hz4) * 2 * M, 16);
+  l.pf = o; o = align_up(o + sizeof(Pf3) * 2 * M, 16);
+  l.ering = o; o = align_up(o + sizeof(double) * 2 * kEBlock * 2 * K, 16);
+  l.cl = o; o = align_up(o + sizeof(ConstLds), 16);
   l.parents = o; o = align_up(o + sizeof(int) * (M > B ? M : B), 16);
-  l.sysp = o; o = align_up(o + sizeof(int) * M, 16);
   l.X = o; o = align_up(o + sizeof(uint64_t) * B, 16);
   l.grp = o; o = align_up(o + sizeof(int) * B, 16);
   l.gst = o; o = align_up(o + sizeof(uint64_t) * B, 16);
-  l.red = o; o = align_up(o + 128, 16);
+  l.red = o; o = align_up(o + 32 * (NT / 64), 16);
   l.sh = o; o = align_up(o + sizeof(Shared), 16);
   l.total = o;
   return l;
 }
 
 // ---------------------------------------------------------- shared steps
-// Stage emission rows [bi*EB, min(bi*EB+EB, T)) of the chain into the ring.
-__device__ __forceinline__ void load_eblock(double* ering, const double* __restrict__ Ech, int bi, int T, int K2) {
+// Emission rows live in a 2 x kEBlock ring: row t at ring[((t/EB)&1)*EB + t%EB].
+__device__ __forceinline__ void load_eblock(double* ering, const double* __restrict__ Ech, int bi, int T, int K2,
+                                            int NT) {
   const int t0 = bi * kEBlock;
+  if (t0 >= T) return;
   const int rows = (T - t0) < kEBlock ? (T - t0) : kEBlock;
-  const int n = rows * K2;
-  for (int i = threadIdx.x; i < n; i += kThreads) ering[i] = Ech[(size_t)t0 * K2 + i];
+  double* dst = ering + (size_t)(bi & 1) * kEBlock * K2;
+  for (int i = threadIdx.x; i < rows * K2; i += NT) dst[i] = Ech[(size_t)t0 * K2 + i];
+}
+__device__ __forceinline__ const double* erow(const double* ering, int t, int K2) {
+  return ering + ((size_t)((t / kEBlock) & 1) * kEBlock + (t % kEBlock)) * K2;
 }
 
-// Weights of the particles of step t >= 1 from the record (pst, pw, phz and
-// the step scalars); _filter_one_step :235-270 and expand_collapsed_results.
-__device__ __forceinline__ void gen_weights(const hyg_tg_consts* __restrict__ c, int K, int I, int np, int mode,
-                                            float log_c, double lse, const uint64_t* pst, const double* pw,
-                                            const double* phz, const double* Et, double* W) {
+// Weight of particle n of a step t >= 1 from the ancestors (pst, pw, phz) and
+// the step scalars (_filter_one_step :235-270).
+__device__ __forceinline__ double weight_one(const ConstLds& cl, int K, int n, int np, int mode, float log_c,
+                                             double lse, const uint64_t* pst, const double* pw, const Hz4* phz,
+                                             const double* Et) {
+  const int s = fdiv(n, np, 1.0f / (float)np), a = n - s * np;
+  const uint64_t par = pst[a];
+  const uint64_t x = tg_xi(K, par, s);
+  const double tr = tg_trans(cl, K, par, x, phz[a]);
+  if (!hyg_isfinite(tr)) return HYG_NINF;
+  const double lg = tr + (Et[hyg_st_rc(x)] + Et[K + hyg_st_rk(x)]);
+  const double pa = pw[a];
+  if (mode == MODE_KEEP) return pa + lg;
+  if (mode == MODE_UNBIASED) return (-cl.log_M + lse) + lg;
+  const double v = (double)log_c + (pa - lse);
+  return (pa + lg) - (v < 0.0 ? v : 0.0);
+}
+
+// All weights of a step t >= 1; returns this thread's max and count of finite weights.
+template <int NT>
+__device__ __forceinline__ void gen_weights(const ConstLds& cl, int K, int I, int np, int mode, float log_c,
+                                            double lse, const uint64_t* pst, const double* pw, const Hz4* phz,
+                                            const double* Et, double* W, double* m_out, int* c_out) {
   const int N = I * np;
-  for (int n = threadIdx.x; n < N; n += kThreads) {
-    const int s = n / np, a = n - s * np;
-    const uint64_t par = pst[a];
-    const uint64_t x = tg_xi(K, par, s);
-    Hz4 h;
-    h.lrc = phz[4 * a + 0]; h.l1c = phz[4 * a + 1]; h.lrk = phz[4 * a + 2]; h.l1k = phz[4 * a + 3];
-    const double tr = tg_trans(c, K, par, x, h);
-    double w;
-    if (!hyg_isfinite(tr)) {
-      w = HYG_NINF;
-    } else {
-      const double lg = tr + (Et[hyg_st_rc(x)] + Et[K + hyg_st_rk(x)]);
-      if (mode == MODE_KEEP) {
-        w = pw[a] + lg;
-      } else if (mode == MODE_UNBIASED) {
-        w = (-c->log_M + lse) + lg;
-      } else {
-        const double v = (double)log_c + (pw[a] - lse);
-        w = (pw[a] + lg) - (v < 0.0 ? v : 0.0);
-      }
-    }
-    W[n] = w;
-  }
-}
-__device__ __forceinline__ void gen_weights_init(const hyg_tg_consts* __restrict__ c, int K, int r_ph,
-                                                 const double* Et, double* W) {
-  for (int n = threadIdx.x; n < K * K; n += kThreads) {
-    const int i = n / K, j = n - (n / K) * K;
-    const double obs = Et[i] + Et[K + j];
-    const double tr = (i == j) ? c->lPc[r_ph * K + i] : HYG_NINF;
-    W[n] = obs + tr;
-  }
-}
-
-// max and log of the exact mass sum of W[0..N): tf.reduce_logsumexp /
-// tf.nn.log_softmax with the F=100 fixed-point sum of hyg_arith.h.
-__device__ __forceinline__ void lse_block(const double* W, int N, unsigned char* red, double* mx_out,
-                                          double* logS_out, int* cnt_out) {
   double m = HYG_NINF;
   int cnt = 0;
-  for (int n = threadIdx.x; n < N; n += kThreads) {
-    const double w = W[n];
-    m = (w > m) ? w : m;
+  for (int n = threadIdx.x; n < N; n += NT) {
+    const double w = weight_one(cl, K, n, np, mode, log_c, lse, pst, pw, phz, Et);
+    W[n] = w;
+    m = dmax(m, w);
     cnt += (w > HYG_NINF) ? 1 : 0;
   }
-  const double mx = block_max(m, red);
-  const int tot = block_sum(cnt, red);
-  hyg_u128 s = hyg_u128_zero();
-  if (mx > HYG_NINF) {
-    for (int n = threadIdx.x; n < N; n += kThreads) {
-      const double x = W[n] - mx;
-      if (x >= -70.0) s = hyg_u128_add(s, hyg_fix100(hyg_exp(x)));  // exp(x < -70) < 2^-100 -> 0
-    }
+  *m_out = m;
+  *c_out = cnt;
+}
+template <int NT>
+__device__ __forceinline__ void gen_weights_init(const ConstLds& cl, int K, int r_ph, const double* Et, double* W,
+                                                 double* m_out, int* c_out) {
+  double m = HYG_NINF;
+  int cnt = 0;
+  for (int n = threadIdx.x; n < K * K; n += NT) {
+    const int i = n / K, j = n - (n / K) * K;
+    const double obs = Et[i] + Et[K + j];
+    const double tr = (i == j) ? cl.lPc[r_ph * K + i] : HYG_NINF;
+    const double w = obs + tr;
+    W[n] = w;
+    m = dmax(m, w);
+    cnt += (w > HYG_NINF) ? 1 : 0;
   }
-  const hyg_u128 S = block_sum128(s, red);
-  *mx_out = mx;
-  *logS_out = hyg_log(hyg_u128_to_f64(S, 100));
-  *cnt_out = tot;
+  *m_out = m;
+  *c_out = cnt;
 }
 
-// Categorical draws (tfd.Categorical(logits).sample, TF multinomial CDF
-// semantics): for each draw q in [0, n_draw) with random bits rnd(q), the
-// first n with cdf_n > floor(u * total). logits(n) is recomputed on demand.
-template <typename LogitFn, typename ActiveFn, typename RandFn, typename OutFn>
+// log of the exact F=100 mass sum of exp(W - mx) over W[0..N).
+template <int NT>
+__device__ __forceinline__ double log_mass_sum(const double* W, int N, double mx, unsigned char* red) {
+  hyg_u128 s = hyg_u128_zero();
+#pragma unroll 4
+  for (int n = threadIdx.x; n < N; n += NT) {
+    const double x = W[n] - mx;
+    if (x >= -70.0) s = hyg_u128_add(s, hyg_fix100(hyg_exp(x)));  // exp(x < -70) < 2^-100 -> 0
+  }
+  const hyg_u128 S = block_sum128<NT>(s, red);
+  return hyg_log(hyg_u128_to_f64(S, 100));
+}
+
+// Categorical draws (tfd.Categorical(logits).sample with TF's multinomial CDF
+// semantics): for each active draw q with random bits rnd(q), the first n with
+// cdf_n > floor(u * total). logit(n) is recomputed on demand.
+template <int NT, typename LogitFn, typename ActiveFn, typename RandFn, typename OutFn>
 __device__ __forceinline__ void categorical_block(int N, double lmax, LogitFn logit, int n_draw, ActiveFn active,
                                                   RandFn rnd, OutFn out, hyg_u128* cp, unsigned char* red) {
-  const int cs = (N + kThreads - 1) / kThreads;
+  const int cs = (N + NT - 1) / NT;
   const int p0 = threadIdx.x * cs, p1 = (p0 + cs < N) ? p0 + cs : N;
   hyg_u128 loc = hyg_u128_zero();
   for (int n = p0; n < p1; ++n) {
     const double x = logit(n) - lmax;
     if (x >= -70.0) loc = hyg_u128_add(loc, hyg_fix100(hyg_exp(x)));
   }
-  block_scan128(loc, cp, red);
+  block_scan128<NT>(loc, cp, red);
   __syncthreads();
-  const hyg_u128 total = cp[kThreads];
-  for (int q = threadIdx.x; q < n_draw; q += kThreads) {
+  const hyg_u128 total = cp[NT];
+  for (int q = threadIdx.x; q < n_draw; q += NT) {
     if (!active(q)) continue;
     const hyg_u128 target = hyg_scale_target(rnd(q), total);
-    // chunk: last ch with cp[ch] <= target (cp is the exclusive prefix)
-    int lo = 0, hi = kThreads - 1;
+    int lo = 0, hi = NT - 1;  // last chunk with cp[ch] <= target
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (hyg_u128_lt(target, cp[mid])) hi = mid - 1; else lo = mid;
     }
-    // skip empty chunks whose prefix equals the target (first n with cdf > target)
-    int ch = lo;
-    hyg_u128 cdf = cp[ch];
     int sel = -1;
-    for (; ch < kThreads && sel < 0; ++ch) {
-      cdf = cp[ch];
+    for (int ch = lo; ch < NT && sel < 0; ++ch) {
+      hyg_u128 cdf = cp[ch];
       const int a0 = ch * cs, a1 = (a0 + cs < N) ? a0 + cs : N;
       for (int n = a0; n < a1; ++n) {
         const double x = logit(n) - lmax;
@@ -385,8 +495,243 @@ __device__ __forceinline__ void categorical_block(int N, double lmax, LogitFn lo
   }
 }
 
+// ------------------------------------------------------ optimal resampling
+// OptimalFiniteState (resampling_functions.py:7-52) on the significant
+// log-weights (weights below sig_thresh have zero f32 mass and can
+// never be counted by the K search):
+//  1. counting sort: buckets by a monotone map of the f32 value, then each key
+//     is ranked inside its bucket; the sorted order is unique (value desc,
+//     index asc), so the bucket map only affects speed;
+//  2. exact 192-bit mass prefix sums of the sorted masses;
+//  3. the K / log c loop (:12-23): log c(a) and the prefix count P(c(a)) are
+//     evaluated for every a < M at once (one lane per a), then the loop's
+//     iterates a' = max(a, P(c(a))) are followed;
+//  4. the systematic residual draw (:32-40, :56-69): target j lands on the
+//     first residual position with C >= ceil(T_j R) (exact), found by the
+//     thread whose chunk of sorted positions contains it.
+// Writes parents[0..M) and sh.Kk / sh.log_c (log_c not finite -> caller
+// runs the unbiased fallback). Returns n_sig via sh.n_sig.
+template <int NT>
+__device__ void optimal_resample(const double* W, uint64_t* sorted, int N, double mx, double logS, float thr,
+                                 uint64_t* keys, int* bcnt, int* bpos, hyg_u192* pre64, hyg_u192* tau, int* parents,
+                                 Shared& sh,
+                                 const ConstLds& cl, unsigned char* red, int M, int cnt_fin, uint64_t seed,
+                                 uint64_t chain_id, int t, unsigned long long* ph, bool timed) {
+  const int tid = threadIdx.x;
+#define SPH(k)                                                     \
+  if (timed && tid == 0) {                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    ph[k] += now_ - ph[23];                                        \
+    ph[23] = now_;                                                 \
+  }
+  const float scale = (float)kBuckets / (-thr);
+  auto bucket_of = [&](float lw) -> int {
+    const int q = (int)((-lw) * scale);
+    return q < kBuckets - 1 ? q : kBuckets - 1;
+  };
+  // ---- 1a. bucket histogram
+  for (int i = tid; i < kBuckets; i += NT) bcnt[i] = 0;
+  __syncthreads();
+  for (int n = tid; n < N; n += NT) {
+    const double w = W[n];
+    if (w > HYG_NINF) {
+      const float lw = (float)((w - mx) - logS);
+      if (lw >= thr) atomicAdd(&bcnt[bucket_of(lw)], 1);
+    }
+  }
+  __syncthreads();
+  SPH(17);
+  // ---- 1b. bucket starts (exclusive scan), kBuckets / NT buckets per thread
+  {
+    constexpr int PB = (kBuckets + NT - 1) / NT;
+    int loc = 0;
+    for (int i = 0; i < PB; ++i) {
+      const int q = tid * PB + i;
+      if (q < kBuckets) loc += bcnt[q];
+    }
+    int tot;
+    int run = block_excl_int<NT>(loc, red, &tot);
+    for (int i = 0; i < PB; ++i) {
+      const int q = tid * PB + i;
+      if (q < kBuckets) { bpos[q] = run; run += bcnt[q]; }
+    }
+    if (tid == 0) sh.n_sig = tot;
+  }
+  __syncthreads();
+  SPH(18);
+  const int n_sig = sh.n_sig;
+  // ---- 1c. scatter into buckets (arbitrary order inside a bucket)
+  for (int n = tid; n < N; n += NT) {
+    const double w = W[n];
+    if (w > HYG_NINF) {
+      const float lw = (float)((w - mx) - logS);
+      if (lw >= thr) keys[atomicAdd(&bpos[bucket_of(lw)], 1)] = sort_key(lw, n);
+    }
+  }
+  __syncthreads();
+  SPH(19);
+  // ---- 1d. rank every key inside its bucket and place it in `sorted` (the
+  //          W area: every read of W is done); bpos now holds the bucket ends
+  for (int p = tid; p < n_sig; p += NT) {
+    const uint64_t k = keys[p];
+    const int q = bucket_of(key_value(k));
+    const int end = bpos[q], beg = end - bcnt[q];
+    int rank = 0;
+    for (int i = beg; i < end; ++i) rank += (keys[i] < k) ? 1 : 0;
+    sorted[beg + rank] = k;
+  }
+  __syncthreads();
+  SPH(13);
+  // ---- 2. masses and exact prefix sums over contiguous chunks of sorted positions
+  const int cs = (n_sig + NT - 1) / NT;
+  const int p0 = tid * cs;
+  const int p1 = (p0 + cs < n_sig) ? p0 + cs : n_sig;
+  hyg_u192 loc = hyg_u192_zero();
+  for (int p = p0; p < p1; ++p) loc = hyg_u192_add(loc, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
+  hyg_u192 total;
+  const hyg_u192 myex = block_excl192<NT>(loc, red, &total);
+  if (p0 < 64) {  // inclusive prefix of the first 64 sorted positions
+    hyg_u192 run = myex;
+    for (int p = p0; p < p1 && p < 64; ++p) {
+      run = hyg_u192_add(run, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
+      pre64[p] = run;
+    }
+  }
+  __syncthreads();
+  SPH(14);
+  // ---- 3. K / log c (loop-variable semantics of :12-31)
+  if (wave_id() == 0) {
+    const int lane = lane_id();
+    if (M <= 64) {
+      // lane a: c(a) and the prefix count P(c(a)) = #{p : fl(c(a) + x_p) > 0}
+      int Pa = 0;
+      float ca = 0.0f;
+      hyg_u192 rva = hyg_u192_zero();
+      const int a = lane;
+      if (a < M && a < N) {
+        if (a < n_sig) rva = hyg_u192_sub(total, a == 0 ? hyg_u192_zero() : pre64[a - 1]);
+        const double rvd = hyg_u192_to_f64(rva);
+        const float l2 = (rvd == 0.0) ? HYG_NINFF : (float)hyg_log(rvd);
+        ca = cl.logMa[a] - l2;
+        if (hyg_isfinitef(ca)) {
+          int lo = 0, hi = n_sig;  // first p with the predicate false
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((float)(ca + key_value(sorted[mid])) > 0.0f) lo = mid + 1; else hi = mid;
+          }
+          Pa = lo;
+        } else if (ca > 0.0f) {
+          Pa = cnt_fin;  // +inf: every finite particle
+        } else {
+          Pa = 0;
+        }
+      }
+      // follow a <- max(a, P(c(a))) from a = 0 (the body runs at least once)
+      int aa = 0, bb = -1;
+      while (aa != bb && aa < N && aa < M) {
+        const int nxt = __shfl(Pa, aa);
+        bb = aa;
+        aa = nxt > aa ? nxt : aa;
+      }
+      const float lc = __shfl(ca, bb);
+      hyg_u192 R;
+      R.w0 = __shfl(rva.w0, bb);
+      R.w1 = __shfl(rva.w1, bb);
+      R.w2 = __shfl(rva.w2, bb);
+      if (lane == 0) {
+        sh.Kk = bb;
+        sh.log_c = lc;
+        sh.R = R;
+        sh.preK = hyg_u192_sub(total, R);
+      }
+    } else {
+      // general M: the loop as written, one iteration at a time
+      int a = 0, b = -1;
+      float lc = -1.0f;
+      hyg_u192 rv_last = hyg_u192_zero();
+      while (a != b && a < N && a < M) {
+        hyg_u192 rv = hyg_u192_zero();
+        if (a < n_sig) {
+          hyg_u192 pre = hyg_u192_zero();
+          if (a > 0 && a <= 64) pre = pre64[a - 1];
+          else if (a > 64) {
+            pre = pre64[63];
+            for (int p = 64; p < a; ++p) pre = hyg_u192_add(pre, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
+          }
+          rv = hyg_u192_sub(total, pre);
+        }
+        const double rvd = hyg_u192_to_f64(rv);
+        const float l1 = hyg_logf((float)(M - a));
+        const float l2 = (rvd == 0.0) ? HYG_NINFF : (float)hyg_log(rvd);
+        const float cn = l1 - l2;
+        int cnt = 0;
+        if (hyg_isfinitef(cn)) {
+          int lo = 0, hi = n_sig;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((float)(cn + key_value(sorted[mid])) > 0.0f) lo = mid + 1; else hi = mid;
+          }
+          cnt = (lo - a) > 0 ? lo - a : 0;
+        } else if (cn > 0.0f) {
+          cnt = (cnt_fin - a) > 0 ? cnt_fin - a : 0;
+        }
+        b = a;
+        a = a + cnt;
+        lc = cn;
+        rv_last = rv;
+      }
+      if (lane == 0) {
+        sh.Kk = b;
+        sh.log_c = lc;
+        sh.R = rv_last;
+        sh.preK = hyg_u192_sub(total, rv_last);
+      }
+    }
+  }
+  __syncthreads();
+  SPH(15);
+  int Kk = sh.Kk;
+  const float log_c = sh.log_c;
+  if (Kk >= N || !hyg_isfinitef(log_c)) return;  // caller runs the unbiased fallback
+  // ---- 4. deterministic top-K, systematic residual with exact thresholds
+  const int L = M - Kk;
+  const float U = hyg_u01f(hyg_rand64(seed, chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)t, 0));
+  const float Lf = (float)L;
+  const hyg_u192 R = sh.R, preK = sh.preK;
+  for (int j = tid; j < L; j += NT) {
+    tau[j] = hyg_u192_add(preK, hyg_ceil_mul_f32(((float)j + U) / Lf, R));
+    parents[Kk + j] = key_index(sorted[Kk]);  // unfilled -> residual index 0
+  }
+  for (int p = tid; p < Kk; p += NT) parents[p] = key_index(sorted[p]);
+  __syncthreads();
+  if (p0 < n_sig && p0 + cs > Kk && L > 0) {
+    // first target not reached before this chunk: #{j : tau_j <= C(p0 - 1)}
+    int j = 0;
+    if (p0 > Kk) {
+      int lo = 0, hi = L;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (hyg_u192_ge(myex, tau[mid])) lo = mid + 1; else hi = mid;
+      }
+      j = lo;
+    }
+    hyg_u192 C = myex;
+    for (int p = p0; p < p1 && j < L; ++p) {
+      C = hyg_u192_add(C, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
+      if (p >= Kk) {
+        while (j < L && hyg_u192_ge(C, tau[j])) {
+          parents[Kk + j] = key_index(sorted[p]);
+          ++j;
+        }
+      }
+    }
+  }
+  SPH(16);
+#undef SPH
+}
+
 // --------------------------------------------------------------- kernels
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(256)
 tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg, const double* __restrict__ cst,
                    int L, int K, const uint16_t* __restrict__ meth_c, const uint16_t* __restrict__ tot_c, int s_c,
                    const uint16_t* __restrict__ meth_k, const uint16_t* __restrict__ tot_k, int s_k, int64_t T,
@@ -399,7 +744,7 @@ tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
       double e[HYG_KMAX];
       for (int r = 0; r < K; ++r) e[r] = 0.0;
       for (int s = 0; s < S; ++s) {
-        int n = nt[s], y = my[s];
+        const int n = nt[s], y = my[s];
         if (n == 0) continue;
         if (y > n || n >= L) {  // invalid input: poison the row
           for (int r = 0; r < K; ++r) e[r] = HYG_NAN;
@@ -420,10 +765,11 @@ tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
   }
 }
 
-__global__ void __launch_bounds__(kThreads)
+template <int NT>
+__global__ void __launch_bounds__(NT)
 tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                   uint8_t* __restrict__ ws, int32_t* status_out, double* __restrict__ logz_out,
-                  double* __restrict__ finalw_out, Lay lay) {
+                  double* __restrict__ finalw_out, Lay lay, unsigned long long* __restrict__ dbg) {
   const hyg_tg_consts* __restrict__ c = md.consts;
   const int K = c->K, M = c->M, I = c->I, K2 = 2 * K, tid = threadIdx.x;
   const ChainDev ch = chains[blockIdx.x];
@@ -431,24 +777,39 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
   extern __shared__ __align__(16) unsigned char smem[];
   double* W = (double*)(smem + lay.W);
   uint64_t* keys = (uint64_t*)(smem + lay.keys);
-  float* mass = (float*)(smem + lay.mass);
+  hyg_u128* cp128 = (hyg_u128*)(smem + lay.keys);  // prefix arrays of the keep / fallback paths
+  int* bcnt = (int*)(smem + lay.bcnt);
+  int* bpos = (int*)(smem + lay.bpos);
+  hyg_u192* tau = (hyg_u192*)(smem + lay.bcnt);
+  hyg_u192* pre64 = (hyg_u192*)(smem + lay.pre64);
   uint64_t* pst = (uint64_t*)(smem + lay.pst);
   double* pw = (double*)(smem + lay.pw);
-  double* phz = (double*)(smem + lay.phz);
+  Hz4* phz = (Hz4*)(smem + lay.phz);
+  Pf3* pf = (Pf3*)(smem + lay.pf);
   double* ering = (double*)(smem + lay.ering);
-  hyg_u192* cp = (hyg_u192*)(smem + lay.cp);
-  hyg_u128* cp128 = (hyg_u128*)(smem + lay.cp);
+  ConstLds& cl = *(ConstLds*)(smem + lay.cl);
   int* parents = (int*)(smem + lay.parents);
-  int* sysp = (int*)(smem + lay.sysp);
   unsigned char* red = smem + lay.red;
   Shared& sh = *(Shared*)(smem + lay.sh);
+
+  // phase timers (diagnostic runs only: dbg != nullptr), kept in LDS
+  unsigned long long* ph_acc = sh.ph;
+  if (tid < 24) ph_acc[tid] = 0;
+#define PH(k)                                                      \
+  if (dbg && tid == 0) {                                           \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    ph_acc[k] += now_ - ph_acc[23];                                \
+    ph_acc[23] = now_;                                             \
+  }
 
   uint8_t* rec0 = ws + ch.ws_offset;
   const size_t rstride = record_bytes(M);
   const double* Ech = E + ch.site_begin * K2;
 
   // ---- t = 0 (_filter_first_step)
-  load_eblock(ering, Ech, 0, T, K2);
+  load_consts(cl, c, md);
+  load_eblock(ering, Ech, 0, T, K2, NT);
+  load_eblock(ering, Ech, 1, T, K2, NT);
   if (tid == 0) {
     sh.r_ph = (int)hyg_mulhi64(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_PHANTOM, 0, 0), (uint64_t)K);
     sh.status = HYG_OK;
@@ -456,134 +817,73 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     s0->mode = MODE_INIT; s0->n_par = 0; s0->log_c = 0.0f; s0->r_ph = sh.r_ph; s0->lse = 0.0; s0->pad = 0.0;
   }
   __syncthreads();
-  gen_weights_init(c, K, sh.r_ph, ering, W);
+  double mloc;
+  int cloc;
+  gen_weights_init<NT>(cl, K, sh.r_ph, erow(ering, 0, K2), W, &mloc, &cloc);
   int N = K * K, np_prev = 0, prev_mode = MODE_INIT, cur = 0;
-  __syncthreads();
+  float prev_logc = 0.0f;
+  double prev_lse = 0.0;
+  double mx;
+  int cnt;
+  block_max_cnt<NT>(mloc, cloc, red, &mx, &cnt);
 
+  if (dbg && tid == 0) ph_acc[23] = __builtin_amdgcn_s_memtime();
   for (int t = 1; t < T; ++t) {
-    if ((t % kEBlock) == 0) load_eblock(ering, Ech, t / kEBlock, T, K2);  // read after later barriers
-    // ---- weights of step t-1: max, count, log-sum-exp
-    double mx, logS;
-    int cnt;
-    lse_block(W, N, red, &mx, &logS, &cnt);
+    // emission rows one block ahead: issue at the block start, land in the ring later
+    const bool eload = ((t % kEBlock) == 0) && (t + kEBlock < T);
+    PH(0);
     if (!(mx > HYG_NINF)) {
       if (tid == 0) sh.status = HYG_ENUMERIC;
       break;  // uniform
     }
+    // ---- log_softmax / reduce_logsumexp of the weights of step t-1
+    const double logS = log_mass_sum<NT>(W, N, mx, red);
     const double lse = logS + mx;
+    PH(1);
     int mode, np;
     float log_c = 0.0f;
     if (cnt <= M) {
-      // ---- keep every particle with non-zero weight, in index order
+      // ---- keep every particle with non-zero weight, in index order (:207-209)
       mode = MODE_KEEP;
       np = cnt;
-      const int cs = (N + kThreads - 1) / kThreads;
+      const int cs = (N + NT - 1) / NT;
       const int p0 = tid * cs, p1 = (p0 + cs < N) ? p0 + cs : N;
       int loc = 0;
       for (int n = p0; n < p1; ++n) loc += (W[n] > HYG_NINF);
-      // exclusive scan of counts via the u128 scan (values are small)
-      hyg_u128 v; v.lo = (uint64_t)loc; v.hi = 0;
-      block_scan128(v, cp128, red);
+      hyg_u128 v;
+      v.lo = (uint64_t)loc;
+      v.hi = 0;
+      block_scan128<NT>(v, cp128, red);
       __syncthreads();
       int o = (int)cp128[tid].lo;
       for (int n = p0; n < p1; ++n)
         if (W[n] > HYG_NINF) parents[o++] = n;
+      PH(2);
+      if (dbg && tid == 0) ph_acc[10]++;
     } else {
       // ---- OptimalFiniteState (resampling_functions.py:7-52)
-      if (tid == 0) sh.sig_ctr = 0;
-      __syncthreads();
-      const float thr = c->sig_thresh;
-      const int iters = (N + kThreads - 1) / kThreads;
-      for (int it = 0; it < iters; ++it) {
-        const int n = it * kThreads + tid;
-        bool sig = false;
-        uint64_t key = 0;
-        if (n < N) {
-          const double w = W[n];
-          if (w > HYG_NINF) {
-            const float lw = (float)((w - mx) - logS);
-            if (lw >= thr) { sig = true; key = sort_key(lw, n); }
-          }
-        }
-        const unsigned long long mask = __ballot(sig);
-        const int pc = __popcll(mask);
-        unsigned base = 0;
-        if (lane_id() == 0 && pc) base = atomicAdd(&sh.sig_ctr, (unsigned)pc);
-        base = __shfl(base, 0);
-        if (sig) keys[base + __popcll(mask & ((1ull << lane_id()) - 1ull))] = key;
-      }
-      __syncthreads();
-      const int n_sig = (int)sh.sig_ctr;
-      const int n2 = next_pow2(n_sig < 64 ? 64 : n_sig);
-      for (int i = n_sig + tid; i < n2; i += kThreads) keys[i] = ~0ull;
-      __syncthreads();
-      // bitonic sort of keys[0, n2)
-      for (int k = 2; k <= n2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = tid; i < (n2 >> 1); i += kThreads) {
-            const int lo = 2 * j * (i / j) + (i % j);
-            const int hi = lo + j;
-            const uint64_t a = keys[lo], b = keys[hi];
-            const bool up = (lo & k) == 0;
-            if ((a > b) == up) { keys[lo] = b; keys[hi] = a; }
-          }
-          __syncthreads();
-        }
-      }
-      // masses and exact chunk prefix sums over the sorted significant set
-      const int cs = (n_sig + kThreads - 1) / kThreads;
-      {
-        const int p0 = tid * cs, p1 = (p0 + cs < n_sig) ? p0 + cs : n_sig;
-        hyg_u192 loc = hyg_u192_zero();
-        for (int p = p0; p < p1; ++p) {
-          const float m = hyg_expf(key_value(keys[p]));
-          mass[p] = m;
-          loc = hyg_u192_add(loc, hyg_fix149f(m));
-        }
-        block_scan192(loc, cp, red);
-      }
-      __syncthreads();
-      const hyg_u192 total = cp[kThreads];
-      // iterative K / log c with the TF loop-variable semantics
-      int a = 0, b = -1;
-      float lc = -1.0f;
-      while (a != b && a < N && a < M) {
-        if (tid == 0) {
-          hyg_u192 rv = hyg_u192_zero();
-          if (a < n_sig) {
-            const int chk = a / cs;
-            hyg_u192 pre = cp[chk];
-            for (int p = chk * cs; p < a; ++p) pre = hyg_u192_add(pre, hyg_fix149f(mass[p]));
-            rv = hyg_u192_sub(total, pre);
-          }
-          const double rvd = hyg_u192_to_f64(rv);
-          const float l1 = hyg_logf((float)(M - a));
-          const float l2 = (rvd == 0.0) ? HYG_NINFF : (float)hyg_log(rvd);
-          sh.c_new = l1 - l2;
-        }
-        __syncthreads();
-        const float cn = sh.c_new;
-        int loc = 0;
-        if (hyg_isfinitef(cn)) {
-          const int p0 = tid * cs, p1 = (p0 + cs < n_sig) ? p0 + cs : n_sig;
-          for (int p = (p0 > a ? p0 : a); p < p1; ++p) loc += ((float)(cn + key_value(keys[p])) > 0.0f) ? 1 : 0;
-        } else if (tid == 0 && cn > 0.0f) {
-          loc = (cnt - a) > 0 ? cnt - a : 0;  // +inf: every finite particle at position >= a
-        }
-        const int tot = block_sum(loc, red);
-        b = a;
-        a = a + tot;
-        lc = cn;
-      }
-      int Kk = b;
-      log_c = lc;
+      PH(2);
+      optimal_resample<NT>(W, (uint64_t*)W, N, mx, logS, c->sig_thresh, keys, bcnt, bpos, pre64, tau, parents, sh,
+                           cl, red, M, cnt, ch.seed, ch.chain_id, t, ph_acc, dbg != nullptr);
+      if (dbg && tid == 0) ph_acc[9] += sh.n_sig;
+      PH(3);
+      int Kk = sh.Kk;
+      log_c = sh.log_c;
       if (Kk >= N) { Kk = N; log_c = HYG_NINFF; }
+      np = M;
       if (!hyg_isfinitef(log_c)) {
         // ---- unbiased fallback: M categorical draws from log_weights (:42-47)
         mode = MODE_UNBIASED;
-        np = M;
         log_c = 0.0f;
-        const double lmax = (double)key_value(keys[0]);
+        const double lmax = (double)key_value(((const uint64_t*)W)[0]);
+        __syncthreads();  // the sorted keys in the W area are replaced by the regenerated weights
+        if (prev_mode == MODE_INIT) {
+          gen_weights_init<NT>(cl, K, sh.r_ph, erow(ering, t - 1, K2), W, &mloc, &cloc);
+        } else {
+          gen_weights<NT>(cl, K, I, np_prev, prev_mode, prev_logc, prev_lse, pst + cur * M, pw + cur * M,
+                          phz + cur * M, erow(ering, t - 1, K2), W, &mloc, &cloc);
+        }
+        __syncthreads();
         auto logit = [&](int n) -> double {
           const double w = W[n];
           return (w > HYG_NINF) ? (double)(float)((w - mx) - logS) : HYG_NINF;
@@ -594,106 +894,115 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         auto out = [&](int q, int n) { parents[q] = n; };
         auto all = [](int) { return true; };
         __syncthreads();
-        categorical_block(N, lmax, logit, M, all, rnd, out, cp128, red);
+        categorical_block<NT>(N, lmax, logit, M, all, rnd, out, cp128, red);
       } else {
-        // ---- deterministic top-K plus systematic residual (:32-40, :56-69)
         mode = MODE_OPTIMAL;
-        np = M;
-        const int L = M - Kk;
-        if (tid == 0) {
-          hyg_u192 pre = hyg_u192_zero();
-          if (Kk < n_sig) {
-            const int chk = Kk / cs;
-            pre = cp[chk];
-            for (int p = chk * cs; p < Kk; ++p) pre = hyg_u192_add(pre, hyg_fix149f(mass[p]));
-          } else {
-            pre = total;
-          }
-          sh.preK = pre;
-          sh.R = hyg_u192_sub(total, pre);
-        }
-        for (int p = tid; p < Kk; p += kThreads) parents[p] = key_index(keys[p]);
-        for (int j = tid; j < L; j += kThreads) sysp[j] = Kk;
-        __syncthreads();
-        const double Rd = hyg_u192_to_f64(sh.R);
-        const float U = hyg_u01f(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)t, 0));
-        const float Lf = (float)L;
-        const int p0 = tid * cs, p1 = (p0 + cs < n_sig) ? p0 + cs : n_sig;
-        const int lo = (p0 > Kk) ? p0 : Kk;
-        if (lo < p1 && L > 0) {
-          hyg_u192 C = hyg_u192_zero();
-          int j = 0;
-          if (p0 > Kk) {
-            C = hyg_u192_sub(cp[tid], sh.preK);
-            const double Qprev = hyg_u192_to_f64(C) / Rd;
-            while (j < L && (double)(((float)j + U) / Lf) <= Qprev) ++j;
-          }
-          for (int p = lo; p < p1 && j < L; ++p) {
-            C = hyg_u192_add(C, hyg_fix149f(mass[p]));
-            const double Q = hyg_u192_to_f64(C) / Rd;
-            while (j < L && (double)(((float)j + U) / Lf) <= Q) { sysp[j] = p; ++j; }
-          }
-        }
-        __syncthreads();
-        for (int j = tid; j < L; j += kThreads) parents[Kk + j] = key_index(keys[sysp[j]]);
       }
     }
     __syncthreads();
-    // ---- gather the ancestors (states, weights, hazards) and record them
-    {
-      const int nxt = cur ^ 1;
-      StepScalars* rs = (StepScalars*)(rec0 + (size_t)t * rstride);
-      uint64_t* rst = (uint64_t*)(rs + 1);
-      double* rw = (double*)(rst + M);
-      for (int a = tid; a < np; a += kThreads) {
-        const int n = parents[a];
-        uint64_t s;
-        if (prev_mode == MODE_INIT) {
-          s = init_state(K, n);
-        } else {
-          const int sl = n / np_prev;
-          s = tg_xi(K, pst[cur * M + (n - sl * np_prev)], sl);
-        }
-        const double w = W[n];
-        pst[nxt * M + a] = s;
-        pw[nxt * M + a] = w;
-        rst[a] = s;
-        rw[a] = w;
-        const Hz4 h = hz_of(md, K, s);
-        phz[4 * a + 0] = h.lrc; phz[4 * a + 1] = h.l1c; phz[4 * a + 2] = h.lrk; phz[4 * a + 3] = h.l1k;
+    PH(4);
+    // ---- gather the ancestors (state, weight, own hazards), record them,
+    //      and start the hazard-row prefetch for their children
+    const int nxt = cur ^ 1;
+    StepScalars* rs = (StepScalars*)(rec0 + (size_t)t * rstride);
+    uint64_t* rst = (uint64_t*)(rs + 1);
+    double* rw = (double*)(rst + M);
+    Pf3 pfa;
+    const bool have_pf = tid < np;  // np <= M <= NT: one ancestor per thread
+    if (have_pf) {
+      const int a = tid;
+      const int n = parents[a];
+      uint64_t s;
+      Hz4 h;
+      if (prev_mode == MODE_INIT) {
+        s = init_state(K, n);
+        const double2 hc = cl.hz1[0][hyg_st_rc(s)], hk = cl.hz1[1][hyg_st_rk(s)];
+        h.lrc = hc.x; h.l1c = hc.y; h.lrk = hk.x; h.l1k = hk.y;
+      } else {
+        const int sl = fdiv(n, np_prev, 1.0f / (float)np_prev);
+        const int ao = n - sl * np_prev;
+        const uint64_t anc = pst[cur * M + ao];
+        s = tg_xi(K, anc, sl);
+        h = child_hz(cl, K, anc, sl, pf[cur * M + ao], md);
       }
-      if (tid == 0) {
-        rs->mode = mode; rs->n_par = np; rs->log_c = log_c; rs->r_ph = 0; rs->lse = lse; rs->pad = 0.0;
+      // the weight of candidate n of step t-1, recomputed (the W area may hold the sort)
+      double w;
+      if (prev_mode == MODE_INIT) {
+        const int i = n / K, j = n - (n / K) * K;
+        const double* E0 = erow(ering, 0, K2);
+        w = (E0[i] + E0[K + j]) + ((i == j) ? cl.lPc[sh.r_ph * K + i] : HYG_NINF);
+      } else {
+        w = weight_one(cl, K, n, np_prev, prev_mode, prev_logc, prev_lse, pst + cur * M, pw + cur * M,
+                       phz + cur * M, erow(ering, t - 1, K2));
       }
-      cur = nxt;
-      np_prev = np;
-      prev_mode = mode;
+      pst[nxt * M + a] = s;
+      pw[nxt * M + a] = w;
+      phz[nxt * M + a] = h;
+      rst[a] = s;
+      rw[a] = w;
+      pfa = prefetch_rows(md, K, s);  // in flight during the weights
     }
+    if (tid == 0) {
+      rs->mode = mode; rs->n_par = np; rs->log_c = log_c; rs->r_ph = 0; rs->lse = lse; rs->pad = 0.0;
+    }
+    // emission block prefetch (registers), stored into the ring after the weights
+    double ebuf[4];
+    int e_tot = 0;
+    if (eload) {
+      const int t0 = (t / kEBlock + 1) * kEBlock;
+      const int rows = (T - t0) < kEBlock ? (T - t0) : kEBlock;
+      e_tot = rows * K2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = tid + q * NT;
+        ebuf[q] = (i < e_tot) ? Ech[(size_t)t0 * K2 + i] : 0.0;
+      }
+    }
+    cur = nxt;
+    np_prev = np;
+    prev_mode = mode;
+    prev_logc = log_c;
+    prev_lse = lse;
     __syncthreads();
+    PH(5);
     // ---- propose and weight the particles of step t
-    gen_weights(c, K, I, np, mode, log_c, lse, pst + cur * M, pw + cur * M, phz, ering + (t % kEBlock) * K2, W);
+    gen_weights<NT>(cl, K, I, np, mode, log_c, lse, pst + cur * M, pw + cur * M, phz + cur * M,
+                    erow(ering, t, K2), W, &mloc, &cloc);
     N = I * np;
-    __syncthreads();
+    if (have_pf) pf[cur * M + tid] = pfa;
+    if (eload) {
+      double* dst = ering + (size_t)((t / kEBlock + 1) & 1) * kEBlock * K2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = tid + q * NT;
+        if (i < e_tot) dst[i] = ebuf[q];
+      }
+    }
+    block_max_cnt<NT>(mloc, cloc, red, &mx, &cnt);
+    PH(6);
   }
   // ---- final weights: log normalising constant and run()'s second output
-  double mx, logS;
-  int cnt;
-  lse_block(W, N, red, &mx, &logS, &cnt);
+  double logS = HYG_NINF;
+  if (mx > HYG_NINF) logS = log_mass_sum<NT>(W, N, mx, red);
   if (tid == 0) {
     int st = sh.status;
     if (st == HYG_OK && !(mx > HYG_NINF)) st = HYG_ENUMERIC;
     status_out[blockIdx.x] = st;
     logz_out[blockIdx.x] = logS + mx;
-    // the last record's scalars carry N_{T-1} for the backward pass
   }
   if (finalw_out) {
     const int Nmax = c->Nmax;
-    for (int n = tid; n < Nmax; n += kThreads)
-      finalw_out[(size_t)blockIdx.x * Nmax + n] = (n < N) ? W[n] : HYG_NINF;
+    for (int n = tid; n < Nmax; n += NT) finalw_out[(size_t)blockIdx.x * Nmax + n] = (n < N) ? W[n] : HYG_NINF;
   }
+  if (dbg && tid == 0) {
+    for (int k = 0; k < 23; ++k) dbg[(size_t)blockIdx.x * 24 + k] = ph_acc[k];
+    dbg[(size_t)blockIdx.x * 24 + 23] = (unsigned long long)T;
+  }
+#undef PH
 }
 
-__global__ void __launch_bounds__(kThreads)
+template <int NT>
+__global__ void __launch_bounds__(NT)
 tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                    const uint8_t* __restrict__ ws, const int32_t* status_in, int16_t* __restrict__ o_merged,
                    int16_t* __restrict__ o_control, int16_t* __restrict__ o_case, float* __restrict__ o_split,
@@ -708,8 +1017,10 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   double* Lg = (double*)(smem + lay.L);
   uint64_t* pst = (uint64_t*)(smem + lay.pst);
   double* pw = (double*)(smem + lay.pw);
-  double* phz = (double*)(smem + lay.phz);
+  Hz4* phz = (Hz4*)(smem + lay.phz);
+  Pf3* pf = (Pf3*)(smem + lay.pf);
   double* ering = (double*)(smem + lay.ering);
+  ConstLds& cl = *(ConstLds*)(smem + lay.cl);
   hyg_u128* cp128 = (hyg_u128*)(smem + lay.cp);
   int* idx = (int*)(smem + lay.parents);
   uint64_t* X = (uint64_t*)(smem + lay.X);
@@ -721,48 +1032,116 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   const uint8_t* rec0 = ws + ch.ws_offset;
   const size_t rstride = record_bytes(M);
   const double* Ech = E + ch.site_begin * K2;
+  load_consts(cl, c, md);
   if (tid == 0) sh.status = HYG_OK;
+  // Records are read ahead in two stages: step t consumes record t from LDS,
+  // stores record t-1 (read during step t+1) with its hazard rows (issued at
+  // the top of step t), and issues the read of record t-2.
+  auto rec_ptr = [&](int tt) { return rec0 + (size_t)tt * rstride; };
+  StepScalars s = *(const StepScalars*)rec_ptr(T - 1);
+  if (tid < s.n_par) {
+    const uint64_t* rst = (const uint64_t*)(rec_ptr(T - 1) + sizeof(StepScalars));
+    const uint64_t st = rst[tid];
+    pst[tid] = st;
+    pw[tid] = ((const double*)(rst + M))[tid];
+    const double2 hc = hz_at(md, K, 0, hyg_st_rc(st), hyg_st_dc(st));
+    const double2 hk = hz_at(md, K, 1, hyg_st_rk(st), hyg_st_dk(st));
+    Hz4 h;
+    h.lrc = hc.x; h.l1c = hc.y; h.lrk = hk.x; h.l1k = hk.y;
+    phz[tid] = h;
+    pf[tid] = prefetch_rows(md, K, st);
+  }
+  // stage-1 registers: record t-1
+  StepScalars s1{};
+  uint64_t st1 = 0;
+  double w1 = 0.0;
+  if (T >= 2) {
+    s1 = *(const StepScalars*)rec_ptr(T - 2);
+    if (tid < M) {
+      const uint64_t* rst = (const uint64_t*)(rec_ptr(T - 2) + sizeof(StepScalars));
+      st1 = rst[tid];
+      w1 = ((const double*)(rst + M))[tid];
+    }
+  }
+  {
+    const int bi = (T - 1) / kEBlock;
+    load_eblock(ering, Ech, bi, T, K2, NT);
+    if (bi > 0) load_eblock(ering, Ech, bi - 1, T, K2, NT);
+  }
+  int cur = 0;
+  __syncthreads();
 
   for (int t = T - 1; t >= 0; --t) {
-    if (t == T - 1 || (t % kEBlock) == kEBlock - 1) {
-      __syncthreads();
-      load_eblock(ering, Ech, t / kEBlock, T, K2);
-    }
-    // ---- regenerate the particles of step t from its record
-    const StepScalars* rs = (const StepScalars*)(rec0 + (size_t)t * rstride);
-    const StepScalars s = *rs;
-    const uint64_t* rst = (const uint64_t*)(rs + 1);
-    const double* rw = (const double*)(rst + M);
-    __syncthreads();
-    for (int a = tid; a < s.n_par; a += kThreads) {
-      const uint64_t st = rst[a];
-      pst[a] = st;
-      pw[a] = rw[a];
-      const Hz4 h = hz_of(md, K, st);
-      phz[4 * a + 0] = h.lrc; phz[4 * a + 1] = h.l1c; phz[4 * a + 2] = h.lrk; phz[4 * a + 3] = h.l1k;
-    }
-    __syncthreads();
-    const double* Et = ering + (t % kEBlock) * K2;
+    // ---- regenerate the particles of step t from its record (in LDS buffer cur)
+    const double* Et = erow(ering, t, K2);
+    const int np = s.n_par;
+    const uint64_t* P = pst + cur * M;
+    const Hz4* PHZ = phz + cur * M;
+    const Pf3* PF = pf + cur * M;
+    const float rnp = (np > 0) ? 1.0f / (float)np : 0.0f;
     int N;
+    double mloc;
+    int cloc;
     if (s.mode == MODE_INIT) {
-      gen_weights_init(c, K, s.r_ph, Et, W);
+      gen_weights_init<NT>(cl, K, s.r_ph, Et, W, &mloc, &cloc);
       N = K * K;
     } else {
-      gen_weights(c, K, I, s.n_par, s.mode, s.log_c, s.lse, pst, pw, phz, Et, W);
-      N = I * s.n_par;
+      gen_weights<NT>(cl, K, I, np, s.mode, s.log_c, s.lse, P, pw + cur * M, PHZ, Et, W, &mloc, &cloc);
+      N = I * np;
+    }
+    // ---- hazard rows of record t-1's ancestors (arrived: read during step t+1)
+    double2 h1c = make_double2(0.0, 0.0), h1k = make_double2(0.0, 0.0);
+    Pf3 pf1;
+    const bool have1 = (t > 0) && (tid < s1.n_par);
+    if (have1) {
+      h1c = hz_at(md, K, 0, hyg_st_rc(st1), hyg_st_dc(st1));
+      h1k = hz_at(md, K, 1, hyg_st_rk(st1), hyg_st_dk(st1));
+      pf1 = prefetch_rows(md, K, st1);
+    }
+    // ---- issue the read of record t-2
+    StepScalars s2{};
+    uint64_t st2 = 0;
+    double w2 = 0.0;
+    if (t >= 2) {
+      const uint8_t* rn = rec_ptr(t - 2);
+      s2 = *(const StepScalars*)rn;
+      if (tid < M) {
+        const uint64_t* rst = (const uint64_t*)(rn + sizeof(StepScalars));
+        st2 = rst[tid];
+        w2 = ((const double*)(rst + M))[tid];
+      }
+    }
+    // ---- emission block t/EB - 2 into the half freed after this step
+    const bool eload = (t % kEBlock) == 0 && t >= 2 * kEBlock;
+    double ebuf[4];
+    const int e_tot = eload ? kEBlock * K2 : 0;
+    if (eload) {
+      const int t0 = (t / kEBlock - 2) * kEBlock;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = tid + q * NT;
+        ebuf[q] = (i < e_tot) ? Ech[(size_t)t0 * K2 + i] : 0.0;
+      }
     }
     __syncthreads();
-    const int np = s.n_par;
     auto state_of = [&](int n) -> uint64_t {
       if (s.mode == MODE_INIT) return init_state(K, n);
-      const int sl = n / np;
-      return tg_xi(K, pst[n - sl * np], sl);
+      const int sl = fdiv(n, np, rnp);
+      return tg_xi(K, P[n - sl * np], sl);
+    };
+    auto hz_of_n = [&](int n) -> Hz4 {
+      if (s.mode == MODE_INIT) {
+        const int i = n / K, j = n - (n / K) * K;
+        Hz4 h;
+        h.lrc = cl.hz1[0][i].x; h.l1c = cl.hz1[0][i].y; h.lrk = cl.hz1[1][j].x; h.l1k = cl.hz1[1][j].y;
+        return h;
+      }
+      const int sl = fdiv(n, np, rnp), a = n - sl * np;
+      return child_hz(cl, K, P[a], sl, PF[a], md);
     };
     if (t == T - 1) {
       // ---- B draws from the final weights (:383-385)
-      double m = HYG_NINF;
-      for (int n = tid; n < N; n += kThreads) m = (W[n] > m) ? W[n] : m;
-      const double lmax = block_max(m, red);
+      const double lmax = block_max<NT>(mloc, red);
       if (!(lmax > HYG_NINF)) { if (tid == 0) sh.status = HYG_ENUMERIC; __syncthreads(); break; }
       auto logit = [&](int n) -> double { return W[n]; };
       auto rnd = [&](int q) -> uint64_t {
@@ -771,10 +1150,28 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       auto out = [&](int q, int n) { idx[q] = n; };
       auto all = [](int) { return true; };
       __syncthreads();
-      categorical_block(N, lmax, logit, B, all, rnd, out, cp128, red);
+      categorical_block<NT>(N, lmax, logit, B, all, rnd, out, cp128, red);
     } else {
-      // ---- backward kernel rows (:400-435), one per distinct next state
-      if (tid == 0) {
+      // ---- backward-kernel rows (:400-435), one per distinct next state
+      if (B <= 64) {
+        if (wave_id() == 0) {
+          const int lane = lane_id();
+          int g = -1;
+          if (lane < B) {
+            const uint64_t xb = X[lane];
+            g = lane;
+            for (int q = 0; q < lane; ++q)
+              if (X[q] == xb) { g = q; break; }
+          }
+          const unsigned long long lead = __ballot(lane < B && g == lane);
+          if (lane < B) {
+            const int gi = __popcll(lead & ((1ull << g) - 1ull));  // leaders before this group's leader
+            grp[lane] = gi;
+            if (g == lane) gst[gi] = X[lane];
+          }
+          if (lane == 0) sh.ng = __popcll(lead);
+        }
+      } else if (tid == 0) {
         int ng = 0;
         for (int b = 0; b < B; ++b) {
           int g = 0;
@@ -790,36 +1187,33 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       for (int g = 0; g < ng; ++g) {
         const uint64_t xn = gst[g];
         double m = HYG_NINF;
-        for (int n = tid; n < N; n += kThreads) {
+        for (int n = tid; n < N; n += NT) {
           const double w = W[n];
           double l = HYG_NINF;
           if (w > HYG_NINF) {
             const uint64_t x = state_of(n);
-            const Hz4 h = hz_of(md, K, x);
-            const double f = tg_trans(c, K, x, xn, h);
+            const double f = tg_trans(cl, K, x, xn, hz_of_n(n));
             if (hyg_isfinite(f)) l = f + w;
           }
           Lg[n] = l;
-          m = (l > m) ? l : m;
+          m = dmax(m, l);
         }
-        const double lmax = block_max(m, red);
+        const double lmax = block_max<NT>(m, red);
         if (!(lmax > HYG_NINF)) { fail = true; break; }  // uniform
         auto logit = [&](int n) -> double { return Lg[n]; };
-        // the draws of the trajectories whose next state is group g
         auto in_g = [&](int b) { return grp[b] == g; };
         auto rnd = [&](int b) -> uint64_t {
           return hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
         };
         auto out = [&](int b, int n) { idx[b] = n; };
-        __syncthreads();
-        categorical_block(N, lmax, logit, B, in_g, rnd, out, cp128, red);
+        categorical_block<NT>(N, lmax, logit, B, in_g, rnd, out, cp128, red);
         __syncthreads();
       }
       if (fail) { if (tid == 0) sh.status = HYG_ENUMERIC; __syncthreads(); break; }
     }
     __syncthreads();
     // ---- trajectories and test-function means at t (run_inference_two_groups.py:233-240, 294-314)
-    for (int b = tid; b < B; b += kThreads) {
+    for (int b = tid; b < B; b += NT) {
       const uint64_t x = state_of(idx[b]);
       X[b] = x;
       const size_t o = (size_t)(ch.out_begin + t) * B + b;
@@ -828,6 +1222,24 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       o_control[2 * o + 1] = (int16_t)hyg_st_rc(x);
       o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
       o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
+    }
+    // ---- record t-1 (+ hazard rows) into the other LDS buffer
+    const int nb = cur ^ 1;
+    if (have1) {
+      pst[nb * M + tid] = st1;
+      pw[nb * M + tid] = w1;
+      Hz4 h;
+      h.lrc = h1c.x; h.l1c = h1c.y; h.lrk = h1k.x; h.l1k = h1k.y;
+      phz[nb * M + tid] = h;
+      pf[nb * M + tid] = pf1;
+    }
+    if (eload) {
+      double* dst = ering + (size_t)((t / kEBlock - 2) & 1) * kEBlock * K2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = tid + q * NT;
+        if (i < e_tot) dst[i] = ebuf[q];
+      }
     }
     __syncthreads();
     if (tid < 2 * K + 1) {
@@ -842,6 +1254,11 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       if (tid == 0) o_split[ch.out_begin + t] = v;
       else o_regime[(size_t)(ch.out_begin + t) * K2 + (tid - 1)] = v;
     }
+    s = s1;
+    st1 = st2;
+    w1 = w2;
+    s1 = s2;
+    cur = nb;
   }
   __syncthreads();
   if (tid == 0 && status_out) status_out[blockIdx.x] = sh.status;
@@ -861,6 +1278,14 @@ void ev_record(int k, bool end, hipStream_t s) {
   (void)hipEventRecord(e, s);
   g_ev_used[k] = true;
 }
+int threads_per_chain() {
+  static int nt = [] {
+    const char* v = getenv("HYG_THREADS");
+    const int x = v ? atoi(v) : kDefaultThreads;
+    return (x == 256 || x == 512) ? x : kDefaultThreads;
+  }();
+  return nt;
+}
 }  // namespace
 
 void set_kernel_timing(bool on) { g_timing = on; }
@@ -877,46 +1302,86 @@ int last_kernel_ms(float* out3) {
   return HYG_OK;
 }
 
-size_t forward_lds_bytes(const hyg_tg_consts& c) { return make_layout(c.K, c.M, c.B, c.Nmax, false).total; }
-size_t backward_lds_bytes(const hyg_tg_consts& c) { return make_layout(c.K, c.M, c.B, c.Nmax, true).total; }
+size_t forward_lds_bytes(const hyg_tg_consts& c) {
+  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(), false).total;
+}
+size_t backward_lds_bytes(const hyg_tg_consts& c) {
+  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(), true).total;
+}
 
 int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* meth_c, const uint16_t* tot_c,
                     int s_c, const uint16_t* meth_k, const uint16_t* tot_k, int s_k, int64_t n_sites, double* E,
                     void* stream) {
   if (n_sites <= 0) return HYG_OK;
-  int64_t blocks = (n_sites + kThreads - 1) / kThreads;
+  int64_t blocks = (n_sites + 255) / 256;
   if (blocks > 256 * 16) blocks = 256 * 16;
   ev_record(0, false, (hipStream_t)stream);
-  hipLaunchKernelGGL(tg_emission_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, md.lf, md.lg,
+  hipLaunchKernelGGL(tg_emission_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, md.lf, md.lg,
                      md.cst, md.nmax_reads + 1, c.K, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E);
   ev_record(0, true, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
+}
+
+template <int NT>
+static int launch_chains_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
+                            const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
+  const Lay lf = make_layout(c.K, c.M, c.B, c.Nmax, NT, false);
+  const Lay lb = make_layout(c.K, c.M, c.B, c.Nmax, NT, true);
+  if (lf.total > 160 * 1024 || lb.total > 160 * 1024) return HYG_EUNSUPPORTED;
+  if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
+  if (hipFuncSetAttribute((const void*)tg_forward_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lf.total) != hipSuccess)
+    return HYG_EDEVICE;
+  if (hipFuncSetAttribute((const void*)tg_backward_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lb.total) != hipSuccess)
+    return HYG_EDEVICE;
+  unsigned long long* dbg = nullptr;
+  static const bool want_dbg = getenv("HYG_DEBUG_PHASES") != nullptr;
+  if (want_dbg) (void)hipMalloc((void**)&dbg, sizeof(unsigned long long) * 24 * n_chains);
+  if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * 24 * n_chains, s);
+  ev_record(1, false, s);
+  hipLaunchKernelGGL(tg_forward_kernel<NT>, dim3(n_chains), dim3(NT), lf.total, s, md, chains_dev, E, ws,
+                     out.status, out.log_z, out.final_log_weights, lf, dbg);
+  ev_record(1, true, s);
+  if (hipGetLastError() != hipSuccess) return HYG_EDEVICE;
+  if (dbg) {
+    std::vector<unsigned long long> h((size_t)24 * n_chains);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
+    (void)hipFree(dbg);
+    unsigned long long tot[24] = {0};
+    for (int i = 0; i < n_chains; ++i)
+      for (int k = 0; k < 24; ++k) tot[k] += h[(size_t)i * 24 + k];
+    const double steps = (double)tot[23];
+    fprintf(stderr, "[hyg phases NT=%d] chains=%d steps=%.0f cycles/step:", NT, n_chains, steps);
+    const char* nm[7] = {"top", "lse", "compact", "resample", "fallback", "gather", "weights"};
+    double sum = 0;
+    for (int k = 0; k < 7; ++k) {
+      fprintf(stderr, " %s=%.0f", nm[k], tot[k] / steps);
+      sum += tot[k] / steps;
+    }
+    fprintf(stderr, " total=%.0f | keep_steps=%.0f mean_nsig=%.1f mean_n2=%.1f", sum, (double)tot[10],
+            tot[9] / (steps - tot[10]), tot[11] / (steps - tot[10]));
+    const double opt = steps - tot[10];
+    fprintf(stderr, " | per optimal step: hist=%.0f bscan=%.0f scatter=%.0f bsort=%.0f scan=%.0f kloop=%.0f systematic=%.0f\n",
+            tot[17] / opt, tot[18] / opt, tot[19] / opt, tot[13] / opt, tot[14] / opt, tot[15] / opt, tot[16] / opt);
+  }
+  ev_record(2, false, s);
+  hipLaunchKernelGGL(tg_backward_kernel<NT>, dim3(n_chains), dim3(NT), lb.total, s, md, chains_dev, E,
+                     (const uint8_t*)ws, (const int32_t*)out.status, out.merged, out.control, out.kase,
+                     out.split_probs, out.regime_probs, out.status, lb);
+  ev_record(2, true, s);
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }
 
 int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
                   const double* E, uint8_t* ws, const hyg_tg_outputs& out, void* stream) {
   if (n_chains <= 0) return HYG_OK;
-  const Lay lf = make_layout(c.K, c.M, c.B, c.Nmax, false);
-  const Lay lb = make_layout(c.K, c.M, c.B, c.Nmax, true);
-  if (lf.total > 160 * 1024 || lb.total > 160 * 1024) return HYG_EUNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-  if (hipFuncSetAttribute((const void*)tg_forward_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lf.total) != hipSuccess)
-    return HYG_EDEVICE;
-  if (hipFuncSetAttribute((const void*)tg_backward_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lb.total) != hipSuccess)
-    return HYG_EDEVICE;
-  ev_record(1, false, s);
-  hipLaunchKernelGGL(tg_forward_kernel, dim3(n_chains), dim3(kThreads), lf.total, s, md, chains_dev, E, ws,
-                     out.status, out.log_z, out.final_log_weights, lf);
-  ev_record(1, true, s);
-  if (hipGetLastError() != hipSuccess) return HYG_EDEVICE;
-  ev_record(2, false, s);
-  hipLaunchKernelGGL(tg_backward_kernel, dim3(n_chains), dim3(kThreads), lb.total, s, md, chains_dev, E,
-                     (const uint8_t*)ws, (const int32_t*)out.status, out.merged, out.control, out.kase,
-                     out.split_probs, out.regime_probs, out.status, lb);
-  ev_record(2, true, s);
-  return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
+  switch (threads_per_chain()) {
+    case 256: return launch_chains_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s);
+    default: return launch_chains_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s);
+  }
 }
 
 }  // namespace hyg

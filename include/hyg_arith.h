@@ -275,6 +275,58 @@ HYG_HD double hyg_u192_to_f64(hyg_u192 a) {
   return (double)top * hyg_pow2(sh - 149);
 }
 
+HYG_HD int hyg_u192_ge(hyg_u192 a, hyg_u192 b) {
+  if (a.w2 != b.w2) return a.w2 > b.w2;
+  if (a.w1 != b.w1) return a.w1 > b.w1;
+  return a.w0 >= b.w0;
+}
+
+/* ceil(T * R) for an f32 T in [0, 1] and R < 2^151 (R = value * 2^149 as
+ * above): the smallest integer C with T <= C / R in exact arithmetic. The
+ * systematic resampling comparison T_j <= Q_i = C_i / R
+ * (resampling_functions.py:64) is evaluated as C_i >= ceil(T_j * R). */
+HYG_HD hyg_u192 hyg_ceil_mul_f32(float T, hyg_u192 R) {
+  const uint32_t b = hyg_f32_bits(T);
+  hyg_u192 z = hyg_u192_zero();
+  if (b == 0 || (b >> 31)) return z;
+  const int E = (int)((b >> 23) & 0xff);
+  const uint64_t m = (E == 0) ? (uint64_t)(b & 0x7fffffu) : (uint64_t)((b & 0x7fffffu) | 0x800000u);
+  const int s = (E == 0) ? 149 : 150 - E; /* T = m * 2^-s, s >= 23 for T <= 1 */
+  /* P = m * R (m < 2^24, R < 2^151: P < 2^175) */
+  hyg_u192 P;
+  const uint64_t l0 = m * R.w0, h0 = hyg_mulhi64(m, R.w0);
+  const uint64_t l1 = m * R.w1, h1 = hyg_mulhi64(m, R.w1);
+  const uint64_t l2 = m * R.w2;
+  P.w0 = l0;
+  P.w1 = h0 + l1;
+  const uint64_t c1 = P.w1 < h0 ? 1u : 0u;
+  P.w2 = h1 + l2 + c1;
+  /* ceil(P / 2^s) = (P + 2^s - 1) >> s, s in [23, 149] */
+  hyg_u192 bias = z;
+  if (s < 64) bias.w0 = (1ull << s) - 1ull;
+  else if (s < 128) { bias.w0 = ~0ull; bias.w1 = (s == 64) ? 0 : ((1ull << (s - 64)) - 1ull); }
+  else { bias.w0 = ~0ull; bias.w1 = ~0ull; bias.w2 = (s == 128) ? 0 : ((1ull << (s - 128)) - 1ull); }
+  const hyg_u192 Q = hyg_u192_add(P, bias);
+  hyg_u192 r;
+  if (s < 64) {
+    r.w0 = (Q.w0 >> s) | (Q.w1 << (64 - s));
+    r.w1 = (Q.w1 >> s) | (Q.w2 << (64 - s));
+    r.w2 = Q.w2 >> s;
+  } else if (s == 64) {
+    r.w0 = Q.w1; r.w1 = Q.w2; r.w2 = 0;
+  } else if (s < 128) {
+    const int t = s - 64;
+    r.w0 = (Q.w1 >> t) | (Q.w2 << (64 - t));
+    r.w1 = Q.w2 >> t;
+    r.w2 = 0;
+  } else if (s == 128) {
+    r.w0 = Q.w2; r.w1 = 0; r.w2 = 0;
+  } else {
+    r.w0 = Q.w2 >> (s - 128); r.w1 = 0; r.w2 = 0;
+  }
+  return r;
+}
+
 /* ------------------------------------------------------- Philox4x64-10 */
 typedef struct { uint64_t v[4]; } hyg_ph4;
 

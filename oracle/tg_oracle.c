@@ -278,20 +278,19 @@ static int cmp_u64(const void* a, const void* b) {
 }
 
 /* SystematicResampling (resampling_functions.py:56-69) on the residual
- * sorted[K:]: T_j = (j + U)/L in float32, Q = exact cumulative residual mass
- * / residual total; parents[j] = first i with T_j <= Q_i (unfilled -> 0). */
+ * sorted[K:]: T_j = (j + U)/L in float32; Q_i = (exact cumulative residual
+ * mass) / (exact residual total R); parents[j] = first i with T_j <= Q_i,
+ * the comparison evaluated exactly as C_i >= ceil(T_j R) (unfilled -> 0). */
 static void systematic_residual(const float* mass_sorted, int K, int Np, int L, float U, int* out) {
   hyg_u192 R = hyg_u192_zero();
   for (int p = K; p < Np; ++p) R = hyg_u192_add(R, hyg_fix149f(mass_sorted[p]));
-  const double Rd = hyg_u192_to_f64(R);
   for (int j = 0; j < L; ++j) out[j] = 0;
   int i = 0, j = 0;
   hyg_u192 C = hyg_fix149f(mass_sorted[K]);
   const int len = Np - K;
   while (j < L && i < len) {
     const float Tj = ((float)j + U) / (float)L;
-    const double Qi = hyg_u192_to_f64(C) / Rd;
-    if ((double)Tj <= Qi) {
+    if (hyg_u192_ge(C, hyg_ceil_mul_f32(Tj, R))) {
       out[j] = i;
       ++j;
     } else {

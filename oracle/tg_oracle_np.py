@@ -124,6 +124,17 @@ def fix149f(m: np.float32) -> int:
     return mant >> (-sh)
 
 
+def ceil_mul_f32(T: np.float32, R: int) -> int:
+    """ceil(T * R) exactly, for an f32 T (the systematic comparison threshold)."""
+    b = int(np.array(T, dtype=np.float32).view(np.uint32))
+    if b == 0 or (b >> 31):
+        return 0
+    E = (b >> 23) & 0xFF
+    m = (b & 0x7FFFFF) if E == 0 else ((b & 0x7FFFFF) | 0x800000)
+    s = 149 if E == 0 else 150 - E
+    return (m * R + (1 << s) - 1) >> s
+
+
 def int_to_f64(V: int, scale: int) -> float:
     """top 53 bits (truncated) of V, times 2^-scale."""
     if V == 0:
@@ -335,14 +346,13 @@ def run_chain(model: Model, E: np.ndarray, seed: int, chain: int):
                 L = M - Kk
                 parents = order[:Kk]
                 R = revcum[Kk]
-                Rd = int_to_f64(R, 149)
                 U = u01f(rand64(seed, chain, RNG_SYSTEMATIC, t, 0))
                 sys_ = [0] * L
                 i, j, C = 0, 0, ints[Kk]
                 ln = N - Kk
                 while j < L and i < ln:
                     Tj = np.float32((np.float32(j) + U) / np.float32(L))
-                    if float(Tj) <= int_to_f64(C, 149) / Rd:
+                    if C >= ceil_mul_f32(Tj, R):
                         sys_[j] = i
                         j += 1
                     else:
