@@ -946,14 +946,15 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       rs->mode = mode; rs->n_par = np; rs->log_c = log_c; rs->r_ph = 0; rs->lse = lse; rs->pad = 0.0;
     }
     // emission block prefetch (registers), stored into the ring after the weights
-    double ebuf[4];
+    constexpr int EQ = (kEBlock * 2 * HYG_KMAX + NT - 1) / NT;  // rows of one block per thread
+    double ebuf[EQ];
     int e_tot = 0;
     if (eload) {
       const int t0 = (t / kEBlock + 1) * kEBlock;
       const int rows = (T - t0) < kEBlock ? (T - t0) : kEBlock;
       e_tot = rows * K2;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < EQ; ++q) {
         const int i = tid + q * NT;
         ebuf[q] = (i < e_tot) ? Ech[(size_t)t0 * K2 + i] : 0.0;
       }
@@ -973,7 +974,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     if (eload) {
       double* dst = ering + (size_t)((t / kEBlock + 1) & 1) * kEBlock * K2;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < EQ; ++q) {
         const int i = tid + q * NT;
         if (i < e_tot) dst[i] = ebuf[q];
       }
@@ -1113,12 +1114,13 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     }
     // ---- emission block t/EB - 2 into the half freed after this step
     const bool eload = (t % kEBlock) == 0 && t >= 2 * kEBlock;
-    double ebuf[4];
+    constexpr int EQ = (kEBlock * 2 * HYG_KMAX + NT - 1) / NT;  // rows of one block per thread
+    double ebuf[EQ];
     const int e_tot = eload ? kEBlock * K2 : 0;
     if (eload) {
       const int t0 = (t / kEBlock - 2) * kEBlock;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < EQ; ++q) {
         const int i = tid + q * NT;
         ebuf[q] = (i < e_tot) ? Ech[(size_t)t0 * K2 + i] : 0.0;
       }
@@ -1236,7 +1238,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     if (eload) {
       double* dst = ering + (size_t)((t / kEBlock - 2) & 1) * kEBlock * K2;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < EQ; ++q) {
         const int i = tid + q * NT;
         if (i < e_tot) dst[i] = ebuf[q];
       }
@@ -1282,7 +1284,7 @@ int threads_per_chain() {
   static int nt = [] {
     const char* v = getenv("HYG_THREADS");
     const int x = v ? atoi(v) : kDefaultThreads;
-    return (x == 256 || x == 512) ? x : kDefaultThreads;
+    return (x == 64 || x == 128 || x == 256 || x == 512) ? x : kDefaultThreads;
   }();
   return nt;
 }
@@ -1379,6 +1381,8 @@ int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* ch
   if (n_chains <= 0) return HYG_OK;
   hipStream_t s = (hipStream_t)stream;
   switch (threads_per_chain()) {
+    case 64: return launch_chains_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s);
+    case 128: return launch_chains_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s);
     case 256: return launch_chains_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s);
     default: return launch_chains_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s);
   }

@@ -1,0 +1,116 @@
+"""The C-ABI library (include/hygeia_amd.h -> hygeia_amd/lib/libhygeia_amd.so) on a
+host without a GPU: it loads, exports every declared symbol, validates
+parameters, builds the model tables, and refuses to compute (HYG_EDEVICE):
+there is no CPU fallback in the product path.
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from hygeia_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    txt = open(os.path.join(ROOT, "include", "hygeia_amd.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(hyg_[a-z0-9_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    names = _declared()
+    assert len(names) >= 13
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_lib.EXPORTS)
+    assert lib.hyg_version().decode().startswith("hygeia_amd")
+
+
+def test_params_default_matches_reference_flags(lib):
+    p = _lib.TgParams()
+    lib.hyg_tg_params_default(C.byref(p))
+    assert (p.n_regimes, p.minimum_duration, p.num_resampled_ancestors, p.num_samples_backward) == (6, 3, 50, 25)
+    assert p.optimal_resampling == 1 and p.multinomial == 0
+    assert p.omega_case == pytest.approx(0.8)
+    assert p.split_prob == pytest.approx(0.01)
+    assert p.merge_log_prob == pytest.approx(np.log(0.1))
+    assert p.kappa_control == 2.0 and p.kappa_case == 2.0
+
+
+def _params():
+    from hygeia_amd import two_group
+    mu = [0.95, 0.05, 0.8, 0.2, 0.5, 0.5]
+    sg = [0.05, 0.05, 0.1, 0.1, 0.1, 0.2886751]
+    return _lib.make_params(mu, sg, two_group.uniform_theta(6, 0.8))
+
+
+def test_model_create_and_sizes_without_device(lib):
+    m = C.c_void_p()
+    rc = lib.hyg_tg_model_create(C.byref(_params()), 200, 1000, C.byref(m))
+    assert rc == _lib.HYG_OK, lib.hyg_last_error()
+    try:
+        assert lib.hyg_tg_num_particles(m) == 2400
+        ws = lib.hyg_tg_workspace_bytes(m, 3, 1000)
+        assert ws >= 1000 * (32 + 16 * 50)
+    finally:
+        lib.hyg_tg_model_destroy(m)
+
+
+@pytest.mark.parametrize("field,value", [("n_regimes", 1), ("n_regimes", 17), ("num_resampled_ancestors", 0),
+                                         ("num_samples_backward", 0), ("minimum_duration", -1)])
+def test_model_create_rejects_invalid(lib, field, value):
+    p = _params()
+    setattr(p, field, value)
+    m = C.c_void_p()
+    rc = lib.hyg_tg_model_create(C.byref(p), 200, 1000, C.byref(m))
+    assert rc == _lib.HYG_EINVAL
+    assert lib.hyg_last_error()
+
+
+def test_sigma_outside_beta_range_is_rejected(lib):
+    p = _params()
+    p.sigma[0] = 0.6  # nu = mu(1-mu)/sigma^2 - 1 < 0
+    m = C.c_void_p()
+    assert lib.hyg_tg_model_create(C.byref(p), 200, 1000, C.byref(m)) == _lib.HYG_EINVAL
+
+
+@pytest.mark.skipif(_lib.load().hyg_device_count() > 0, reason="host without a GPU only")
+def test_compute_refuses_without_device(lib):
+    m = C.c_void_p()
+    assert lib.hyg_tg_model_create(C.byref(_params()), 200, 1000, C.byref(m)) == _lib.HYG_OK
+    try:
+        T = 10
+        z = np.zeros((T, 2), np.uint16)
+        out = {k: np.zeros(s, dt) for k, s, dt in (("mg", (T, 25), np.int16), ("ct", (T, 25, 2), np.int16),
+                                                   ("ks", (T, 25, 2), np.int16), ("sp", T, np.float32),
+                                                   ("rp", (T, 12), np.float32), ("lz", 1, np.float64))}
+        ptr = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        rc = lib.hyg_tg_run_chain_host(m, ptr(z), ptr(z), 2, ptr(z), ptr(z), 2, T, 0, 0, ptr(out["mg"]),
+                                       ptr(out["ct"]), ptr(out["ks"]), ptr(out["sp"]), ptr(out["rp"]),
+                                       ptr(out["lz"]), None)
+        assert rc == _lib.HYG_EDEVICE
+        assert b"no CPU fallback" in lib.hyg_last_error()
+        E = np.zeros((T, 12))
+        rc = lib.hyg_tg_emission(m, ptr(z), ptr(z), 2, ptr(z), ptr(z), 2, T, ptr(E), None)
+        assert rc == _lib.HYG_EDEVICE
+    finally:
+        lib.hyg_tg_model_destroy(m)
+
+
+def test_product_package_does_not_import_oracle():
+    """The product path must never route through the CPU oracle."""
+    pkg = os.path.join(ROOT, "hygeia_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.sub(r"(#|//).*", "", txt).replace("oracle/", ""), f

@@ -169,3 +169,29 @@ def test_long_chain_properties_and_determinism():
     acc = (rp[:, :6].argmax(1) == d["regime_control"]).mean()
     assert acc > 0.95, acc
     assert np.isfinite(ex["log_z"])
+
+
+@pytest.mark.parametrize("name", ["tg_chain_k6", "tg_chain_k4"])
+def test_golden_fixture(name):
+    """The committed golden fixtures (tests/golden/make_golden.py), through the C ABI."""
+    import os
+
+    from hygeia_amd import two_group
+
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"))
+    K, M, B = int(g["K"]), int(g["M"]), int(g["B"])
+    theta = two_group.uniform_theta(K, 0.8)
+    T = g["tot_control"].shape[0]
+    maxr = int(max(g["tot_control"].max(), g["tot_case"].max()))
+    model = _model(g["mu"], g["sigma"], theta, M, B, maxr, T + 5)
+    res, fw, ex = two_group.run({"control": g["meth_control"], "case": g["meth_case"]},
+                                {"control": g["tot_control"], "case": g["tot_case"]}, model, int(g["seed"]),
+                                int(g["chain_id"]))
+    pr = res.particle
+    np.testing.assert_array_equal(pr["merged_state"], g["merged"])
+    np.testing.assert_array_equal(pr["control_state"], g["control"])
+    np.testing.assert_array_equal(pr["case_state"], g["case"])
+    np.testing.assert_array_equal(ex["split_probs"], g["split_probs"])
+    np.testing.assert_array_equal(ex["regime_probs"], g["regime_probs"])
+    assert ex["log_z"] == float(g["log_z"])
+    np.testing.assert_array_equal(fw, g["final_log_weights"])
