@@ -10,7 +10,7 @@
 namespace hyg {
 
 constexpr int kDefaultThreads = 256;  // threads of the per-chain workgroup (HYG_THREADS overrides)
-constexpr int kEBlock = 16;    // emission rows staged in LDS per block of steps
+constexpr int kEBlock = 8;     // emission rows staged in LDS per block of steps
 
 // Device-side chain descriptor (lives in the workspace header).
 struct ChainDev {

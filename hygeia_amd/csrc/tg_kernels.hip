@@ -198,13 +198,16 @@ struct Hz4 {
 };
 
 struct ConstLds {  // model constants staged in LDS
-  double lPc[HYG_KMAX * HYG_KMAX];
   double lPm[4];
   double lU1, lU2, log_M;
   double2 hz1[2][HYG_KMAX];  // hazard rows at d = 1
   float logMa[64];           // (float)log(M - a) for a < min(M, 64) (resampling_functions.py:13)
   int u, K;
+  double lPc[HYG_KMAX * HYG_KMAX];  // last: only K*K entries are allocated (const_lds_bytes)
 };
+__host__ __device__ inline size_t const_lds_bytes(int K) {
+  return sizeof(ConstLds) - sizeof(double) * (size_t)(HYG_KMAX * HYG_KMAX - K * K);
+}
 
 __device__ __forceinline__ double2 hz_at(const ModelDev& md, int K, int g, int r, int d) {
   d = d < 0 ? 0 : (d >= md.dcap ? md.dcap - 1 : d);
@@ -331,7 +334,7 @@ __host__ __device__ inline int next_pow2(int x) {
   return p;
 }
 
-constexpr int kBuckets = 1024;  // counting-sort buckets of the resampling sort
+constexpr int kBuckets = 512;  // counting-sort buckets of the resampling sort (sqrt-spaced in -lw)
 
 struct Lay {  // byte offsets into the dynamic LDS
   size_t W, L, keys, bcnt, bpos, pre64, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, red, sh, total;
@@ -339,9 +342,10 @@ struct Lay {  // byte offsets into the dynamic LDS
 };
 
 __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT, bool backward) {
+  // Sized for 3 workgroups per CU at K = 6, M = 50, NT = 256 (<= 53 KiB each).
   Lay l{};
   l.nt = NT;
-  l.npad = (int)align_up((size_t)Nmax, NT);
+  l.npad = Nmax;
   size_t o = 0;
   l.W = o; o = align_up(o + sizeof(double) * l.npad, 16);
   if (backward) {
@@ -359,18 +363,21 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
     l.bcnt = o;
     l.bpos = o + sizeof(int) * kBuckets;
     o = align_up(o + bb, 16);
-    l.pre64 = o; o = align_up(o + sizeof(hyg_u192) * 64, 16);
+    l.pre64 = o; o = align_up(o + sizeof(hyg_u192) * (M < 64 ? M : 64), 16);
   }
-  l.pst = o; o = align_up(o + sizeof(uint64_t) * 2 * M, 16);
-  l.pw = o; o = align_up(o + sizeof(double) * 2 * M, 16);
-  l.phz = o; o = align_up(o + sizeof(Hz4) * 2 * M, 16);
-  l.pf = o; o = align_up(o + sizeof(Pf3) * 2 * M, 16);
+  // the ancestors of the current step (single buffer: rewritten behind a barrier)
+  l.pst = o; o = align_up(o + sizeof(uint64_t) * M, 16);
+  l.pw = o; o = align_up(o + sizeof(double) * M, 16);
+  l.phz = o; o = align_up(o + sizeof(Hz4) * M, 16);
+  l.pf = o; o = align_up(o + sizeof(Pf3) * M, 16);
   l.ering = o; o = align_up(o + sizeof(double) * 2 * kEBlock * 2 * K, 16);
-  l.cl = o; o = align_up(o + sizeof(ConstLds), 16);
+  l.cl = o; o = align_up(o + const_lds_bytes(K), 16);
   l.parents = o; o = align_up(o + sizeof(int) * (M > B ? M : B), 16);
-  l.X = o; o = align_up(o + sizeof(uint64_t) * B, 16);
-  l.grp = o; o = align_up(o + sizeof(int) * B, 16);
-  l.gst = o; o = align_up(o + sizeof(uint64_t) * B, 16);
+  if (backward) {
+    l.X = o; o = align_up(o + sizeof(uint64_t) * B, 16);
+    l.grp = o; o = align_up(o + sizeof(int) * B, 16);
+    l.gst = o; o = align_up(o + sizeof(uint64_t) * B, 16);
+  }
   l.red = o; o = align_up(o + 32 * (NT / 64), 16);
   l.sh = o; o = align_up(o + sizeof(Shared), 16);
   l.total = o;
@@ -524,9 +531,11 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
     ph[k] += now_ - ph[23];                                        \
     ph[23] = now_;                                                 \
   }
-  const float scale = (float)kBuckets / (-thr);
+  // any monotone map works (the order inside a bucket is resolved exactly);
+  // sqrt spacing puts narrow buckets where the weights crowd, near the top
+  const float scale = 1.0f / (-thr);
   auto bucket_of = [&](float lw) -> int {
-    const int q = (int)((-lw) * scale);
+    const int q = (int)(__builtin_sqrtf((-lw) * scale) * (float)kBuckets);
     return q < kBuckets - 1 ? q : kBuckets - 1;
   };
   // ---- 1a. bucket histogram
@@ -590,9 +599,10 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
   for (int p = p0; p < p1; ++p) loc = hyg_u192_add(loc, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
   hyg_u192 total;
   const hyg_u192 myex = block_excl192<NT>(loc, red, &total);
-  if (p0 < 64) {  // inclusive prefix of the first 64 sorted positions
+  const int npre = M < 64 ? M : 64;  // pre64 holds min(M, 64) entries (make_layout)
+  if (p0 < npre) {  // inclusive prefix of the first npre sorted positions
     hyg_u192 run = myex;
-    for (int p = p0; p < p1 && p < 64; ++p) {
+    for (int p = p0; p < p1 && p < npre; ++p) {
       run = hyg_u192_add(run, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
       pre64[p] = run;
     }
@@ -820,7 +830,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
   double mloc;
   int cloc;
   gen_weights_init<NT>(cl, K, sh.r_ph, erow(ering, 0, K2), W, &mloc, &cloc);
-  int N = K * K, np_prev = 0, prev_mode = MODE_INIT, cur = 0;
+  int N = K * K, np_prev = 0, prev_mode = MODE_INIT;
   float prev_logc = 0.0f;
   double prev_lse = 0.0;
   double mx;
@@ -880,8 +890,8 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         if (prev_mode == MODE_INIT) {
           gen_weights_init<NT>(cl, K, sh.r_ph, erow(ering, t - 1, K2), W, &mloc, &cloc);
         } else {
-          gen_weights<NT>(cl, K, I, np_prev, prev_mode, prev_logc, prev_lse, pst + cur * M, pw + cur * M,
-                          phz + cur * M, erow(ering, t - 1, K2), W, &mloc, &cloc);
+          gen_weights<NT>(cl, K, I, np_prev, prev_mode, prev_logc, prev_lse, pst, pw, phz, erow(ering, t - 1, K2),
+                          W, &mloc, &cloc);
         }
         __syncthreads();
         auto logit = [&](int n) -> double {
@@ -903,11 +913,13 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     PH(4);
     // ---- gather the ancestors (state, weight, own hazards), record them,
     //      and start the hazard-row prefetch for their children
-    const int nxt = cur ^ 1;
     StepScalars* rs = (StepScalars*)(rec0 + (size_t)t * rstride);
     uint64_t* rst = (uint64_t*)(rs + 1);
     double* rw = (double*)(rst + M);
     Pf3 pfa;
+    uint64_t gs = 0;
+    double gw = 0.0;
+    Hz4 gh{};
     const bool have_pf = tid < np;  // np <= M <= NT: one ancestor per thread
     if (have_pf) {
       const int a = tid;
@@ -921,9 +933,9 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       } else {
         const int sl = fdiv(n, np_prev, 1.0f / (float)np_prev);
         const int ao = n - sl * np_prev;
-        const uint64_t anc = pst[cur * M + ao];
+        const uint64_t anc = pst[ao];
         s = tg_xi(K, anc, sl);
-        h = child_hz(cl, K, anc, sl, pf[cur * M + ao], md);
+        h = child_hz(cl, K, anc, sl, pf[ao], md);
       }
       // the weight of candidate n of step t-1, recomputed (the W area may hold the sort)
       double w;
@@ -932,12 +944,11 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         const double* E0 = erow(ering, 0, K2);
         w = (E0[i] + E0[K + j]) + ((i == j) ? cl.lPc[sh.r_ph * K + i] : HYG_NINF);
       } else {
-        w = weight_one(cl, K, n, np_prev, prev_mode, prev_logc, prev_lse, pst + cur * M, pw + cur * M,
-                       phz + cur * M, erow(ering, t - 1, K2));
+        w = weight_one(cl, K, n, np_prev, prev_mode, prev_logc, prev_lse, pst, pw, phz, erow(ering, t - 1, K2));
       }
-      pst[nxt * M + a] = s;
-      pw[nxt * M + a] = w;
-      phz[nxt * M + a] = h;
+      gs = s;
+      gw = w;
+      gh = h;
       rst[a] = s;
       rw[a] = w;
       pfa = prefetch_rows(md, K, s);  // in flight during the weights
@@ -959,18 +970,23 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         ebuf[q] = (i < e_tot) ? Ech[(size_t)t0 * K2 + i] : 0.0;
       }
     }
-    cur = nxt;
     np_prev = np;
     prev_mode = mode;
     prev_logc = log_c;
     prev_lse = lse;
+    __syncthreads();  // every read of the previous ancestors is done
+    if (have_pf) {
+      pst[tid] = gs;
+      pw[tid] = gw;
+      phz[tid] = gh;
+    }
     __syncthreads();
     PH(5);
     // ---- propose and weight the particles of step t
-    gen_weights<NT>(cl, K, I, np, mode, log_c, lse, pst + cur * M, pw + cur * M, phz + cur * M,
+    gen_weights<NT>(cl, K, I, np, mode, log_c, lse, pst, pw, phz,
                     erow(ering, t, K2), W, &mloc, &cloc);
     N = I * np;
-    if (have_pf) pf[cur * M + tid] = pfa;
+    if (have_pf) pf[tid] = pfa;
     if (eload) {
       double* dst = ering + (size_t)((t / kEBlock + 1) & 1) * kEBlock * K2;
 #pragma unroll
@@ -1069,16 +1085,15 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     load_eblock(ering, Ech, bi, T, K2, NT);
     if (bi > 0) load_eblock(ering, Ech, bi - 1, T, K2, NT);
   }
-  int cur = 0;
   __syncthreads();
 
   for (int t = T - 1; t >= 0; --t) {
-    // ---- regenerate the particles of step t from its record (in LDS buffer cur)
+    // ---- regenerate the particles of step t from its record (in LDS)
     const double* Et = erow(ering, t, K2);
     const int np = s.n_par;
-    const uint64_t* P = pst + cur * M;
-    const Hz4* PHZ = phz + cur * M;
-    const Pf3* PF = pf + cur * M;
+    const uint64_t* P = pst;
+    const Hz4* PHZ = phz;
+    const Pf3* PF = pf;
     const float rnp = (np > 0) ? 1.0f / (float)np : 0.0f;
     int N;
     double mloc;
@@ -1087,7 +1102,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       gen_weights_init<NT>(cl, K, s.r_ph, Et, W, &mloc, &cloc);
       N = K * K;
     } else {
-      gen_weights<NT>(cl, K, I, np, s.mode, s.log_c, s.lse, P, pw + cur * M, PHZ, Et, W, &mloc, &cloc);
+      gen_weights<NT>(cl, K, I, np, s.mode, s.log_c, s.lse, P, pw, PHZ, Et, W, &mloc, &cloc);
       N = I * np;
     }
     // ---- hazard rows of record t-1's ancestors (arrived: read during step t+1)
@@ -1225,15 +1240,15 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
       o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
     }
-    // ---- record t-1 (+ hazard rows) into the other LDS buffer
-    const int nb = cur ^ 1;
+    // ---- record t-1 (+ hazard rows) replaces record t once every read of it is done
+    __syncthreads();
     if (have1) {
-      pst[nb * M + tid] = st1;
-      pw[nb * M + tid] = w1;
+      pst[tid] = st1;
+      pw[tid] = w1;
       Hz4 h;
       h.lrc = h1c.x; h.l1c = h1c.y; h.lrk = h1k.x; h.l1k = h1k.y;
-      phz[nb * M + tid] = h;
-      pf[nb * M + tid] = pf1;
+      phz[tid] = h;
+      pf[tid] = pf1;
     }
     if (eload) {
       double* dst = ering + (size_t)((t / kEBlock - 2) & 1) * kEBlock * K2;
@@ -1260,7 +1275,6 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     st1 = st2;
     w1 = w2;
     s1 = s2;
-    cur = nb;
   }
   __syncthreads();
   if (tid == 0 && status_out) status_out[blockIdx.x] = sh.status;
