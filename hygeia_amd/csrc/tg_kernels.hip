@@ -33,29 +33,136 @@ enum { MODE_KEEP = 0, MODE_OPTIMAL = 1, MODE_UNBIASED = 2, MODE_INIT = 3 };
 
 // ----------------------------------------------------------- small helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// wave index as a wave-uniform (SGPR) value, so branches on it are scalar
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
-__device__ __forceinline__ unsigned long long shx(unsigned long long v, int o) { return __shfl_xor(v, o); }
-__device__ __forceinline__ unsigned long long shu(unsigned long long v, int o) { return __shfl_up(v, o); }
+// Workgroup barrier for LDS hand-offs only. __syncthreads() is a full
+// workgroup fence: it also waits for every outstanding global load and store
+// of the wave (vmcnt(0)), which would stall each step on the ancestor-history
+// stores and on the hazard-row / emission prefetches. Nothing a chain kernel
+// writes to global memory is read back by another wave of the same launch.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// ------------------------------------------------- DPP wave primitives
+// Cross-lane traffic goes through DPP (row shifts / mirrors / broadcasts,
+// a few cycles each) and v_readlane, never ds_bpermute (an LDS round trip
+// per step). Sums are exact integer sums and maxima are exact, so the
+// reduction tree is free.
+enum : int {
+  kDppQuad1032 = 0xB1,      // quad_perm [1,0,3,2]
+  kDppQuad2301 = 0x4E,      // quad_perm [2,3,0,1]
+  kDppRowMirror = 0x140,
+  kDppRowHalfMirror = 0x141,
+  kDppRowBcast15 = 0x142,
+  kDppRowBcast31 = 0x143,
+  kDppRowShr = 0x110,       // + n, n = 1..15
+};
+template <int CTRL, int RM = 0xf, int BM = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  // bound_ctrl: a lane whose source is outside its row reads 0; lanes of
+  // rows disabled by RM keep `old` = 0 as well
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, BM, true);
+}
+template <int CTRL, int RM = 0xf, int BM = 0xf>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const uint32_t lo = dpp32<CTRL, RM, BM>((uint32_t)v), hi = dpp32<CTRL, RM, BM>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double d_of(uint64_t u) { return __builtin_bit_cast(double, u); }
+__device__ __forceinline__ uint64_t u_of(double d) { return __builtin_bit_cast(uint64_t, d); }
 
 __device__ __forceinline__ double dmax(double a, double b) { return (b > a) ? b : a; }
 
-__device__ __forceinline__ double wave_max(double v) {
-  for (int o = 32; o > 0; o >>= 1) v = dmax(v, __shfl_xor(v, o));
+// reduce inside each 16-lane row (every lane of the row gets the row result)
+template <typename F>
+__device__ __forceinline__ double row_reduce_d(double v, F op) {
+  v = op(v, d_of(dpp64<kDppQuad1032>(u_of(v))));
+  v = op(v, d_of(dpp64<kDppQuad2301>(u_of(v))));
+  v = op(v, d_of(dpp64<kDppRowHalfMirror>(u_of(v))));
+  v = op(v, d_of(dpp64<kDppRowMirror>(u_of(v))));
   return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+  auto mx = [](double a, double b) { return dmax(a, b); };
+  v = row_reduce_d(v, mx);
+  const double a = d_of(rdlane64(u_of(v), 0)), b = d_of(rdlane64(u_of(v), 16));
+  const double c = d_of(rdlane64(u_of(v), 32)), d = d_of(rdlane64(u_of(v), 48));
+  return dmax(dmax(a, b), dmax(c, d));
 }
 __device__ __forceinline__ int wave_sum(int v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  uint32_t x = (uint32_t)v;
+  x += dpp32<kDppQuad1032>(x);
+  x += dpp32<kDppQuad2301>(x);
+  x += dpp32<kDppRowHalfMirror>(x);
+  x += dpp32<kDppRowMirror>(x);
+  return __builtin_amdgcn_readlane((int)x, 0) + __builtin_amdgcn_readlane((int)x, 16) +
+         __builtin_amdgcn_readlane((int)x, 32) + __builtin_amdgcn_readlane((int)x, 48);
 }
 __device__ __forceinline__ hyg_u128 wave_sum128(hyg_u128 v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    hyg_u128 w;
-    w.lo = shx(v.lo, o);
-    w.hi = shx(v.hi, o);
-    v = hyg_u128_add(v, w);
+  hyg_u128 w;
+  w.lo = dpp64<kDppQuad1032>(v.lo); w.hi = dpp64<kDppQuad1032>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppQuad2301>(v.lo); w.hi = dpp64<kDppQuad2301>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppRowHalfMirror>(v.lo); w.hi = dpp64<kDppRowHalfMirror>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppRowMirror>(v.lo); w.hi = dpp64<kDppRowMirror>(v.hi); v = hyg_u128_add(v, w);
+  hyg_u128 s = hyg_u128_zero();
+  for (int r = 0; r < 64; r += 16) {
+    hyg_u128 x;
+    x.lo = rdlane64(v.lo, r);
+    x.hi = rdlane64(v.hi, r);
+    s = hyg_u128_add(s, x);
   }
+  return s;
+}
+
+// inclusive wave scans (Hillis-Steele inside rows, then row broadcasts)
+template <int CTRL, int RM>
+__device__ __forceinline__ hyg_u192 dpp192(hyg_u192 v) {
+  hyg_u192 r;
+  r.w0 = dpp64<CTRL, RM>(v.w0); r.w1 = dpp64<CTRL, RM>(v.w1); r.w2 = dpp64<CTRL, RM>(v.w2);
+  return r;
+}
+__device__ __forceinline__ hyg_u192 wave_incl192(hyg_u192 v) {
+  v = hyg_u192_add(v, dpp192<kDppRowShr + 1, 0xf>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowShr + 2, 0xf>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowShr + 4, 0xf>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowShr + 8, 0xf>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowBcast15, 0xa>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowBcast31, 0xc>(v));
   return v;
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ hyg_u128 dpp128(hyg_u128 v) {
+  hyg_u128 r;
+  r.lo = dpp64<CTRL, RM>(v.lo); r.hi = dpp64<CTRL, RM>(v.hi);
+  return r;
+}
+__device__ __forceinline__ hyg_u128 wave_incl128(hyg_u128 v) {
+  v = hyg_u128_add(v, dpp128<kDppRowShr + 1, 0xf>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowShr + 2, 0xf>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowShr + 4, 0xf>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowShr + 8, 0xf>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowBcast15, 0xa>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowBcast31, 0xc>(v));
+  return v;
+}
+__device__ __forceinline__ int wave_incl_int(int v) {
+  uint32_t x = (uint32_t)v;
+  x += dpp32<kDppRowShr + 1, 0xf>(x);
+  x += dpp32<kDppRowShr + 2, 0xf>(x);
+  x += dpp32<kDppRowShr + 4, 0xf>(x);
+  x += dpp32<kDppRowShr + 8, 0xf>(x);
+  x += dpp32<kDppRowBcast15, 0xa>(x);
+  x += dpp32<kDppRowBcast31, 0xc>(x);
+  return (int)x;
 }
 
 // Block-wide reductions. `red` is an LDS scratch of at least 32 B per wave;
@@ -64,12 +171,13 @@ template <int NT>
 __device__ __forceinline__ void block_max_cnt(double m, int c, unsigned char* red, double* m_out, int* c_out) {
   m = wave_max(m);
   c = wave_sum(c);
-  __syncthreads();
+  if (NT == 64) { *m_out = m; *c_out = c; return; }
+  lds_barrier();
   if (lane_id() == 0) {
     ((double*)red)[2 * wave_id()] = m;
     ((int*)red)[4 * wave_id() + 2] = c;
   }
-  __syncthreads();
+  lds_barrier();
   double mm = ((double*)red)[0];
   int cc = ((int*)red)[2];
   for (int w = 1; w < NT / 64; ++w) {
@@ -82,9 +190,10 @@ __device__ __forceinline__ void block_max_cnt(double m, int c, unsigned char* re
 template <int NT>
 __device__ __forceinline__ double block_max(double v, unsigned char* red) {
   v = wave_max(v);
-  __syncthreads();
+  if (NT == 64) return v;
+  lds_barrier();
   if (lane_id() == 0) ((double*)red)[wave_id()] = v;
-  __syncthreads();
+  lds_barrier();
   double m = ((double*)red)[0];
   for (int w = 1; w < NT / 64; ++w) m = dmax(m, ((double*)red)[w]);
   return m;
@@ -93,9 +202,10 @@ template <int NT>
 __device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red) {
   hyg_u128* r = (hyg_u128*)red;
   v = wave_sum128(v);
-  __syncthreads();
+  if (NT == 64) return v;
+  lds_barrier();
   if (lane_id() == 0) r[wave_id()] = v;
-  __syncthreads();
+  lds_barrier();
   hyg_u128 s = hyg_u128_zero();
   for (int w = 0; w < NT / 64; ++w) s = hyg_u128_add(s, r[w]);
   return s;
@@ -107,17 +217,12 @@ __device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red)
 template <int NT>
 __device__ __forceinline__ hyg_u192 block_excl192(hyg_u192 v, unsigned char* red, hyg_u192* total) {
   hyg_u192* r = (hyg_u192*)red;
-  hyg_u192 inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    hyg_u192 n;
-    n.w0 = shu(inc.w0, o);
-    n.w1 = shu(inc.w1, o);
-    n.w2 = shu(inc.w2, o);
-    if (lane_id() >= o) inc = hyg_u192_add(inc, n);
-  }
-  __syncthreads();
-  if (lane_id() == 63) r[wave_id()] = inc;
-  __syncthreads();
+  const hyg_u192 inc = wave_incl192(v);
+  hyg_u192 wt;  // this wave's total
+  wt.w0 = rdlane64(inc.w0, 63); wt.w1 = rdlane64(inc.w1, 63); wt.w2 = rdlane64(inc.w2, 63);
+  lds_barrier();
+  if (lane_id() == 0) r[wave_id()] = wt;
+  lds_barrier();
   hyg_u192 pre = hyg_u192_zero(), tot = hyg_u192_zero();
   for (int w = 0; w < NT / 64; ++w) {
     if (w < wave_id()) pre = hyg_u192_add(pre, r[w]);
@@ -129,14 +234,11 @@ __device__ __forceinline__ hyg_u192 block_excl192(hyg_u192 v, unsigned char* red
 template <int NT>
 __device__ __forceinline__ int block_excl_int(int v, unsigned char* red, int* total) {
   int* r = (int*)red;
-  int inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int n = __shfl_up(inc, o);
-    if (lane_id() >= o) inc += n;
-  }
-  __syncthreads();
-  if (lane_id() == 63) r[wave_id()] = inc;
-  __syncthreads();
+  const int inc = wave_incl_int(v);
+  const int wt = __builtin_amdgcn_readlane(inc, 63);
+  lds_barrier();
+  if (lane_id() == 0) r[wave_id()] = wt;
+  lds_barrier();
   int pre = 0, tot = 0;
   for (int w = 0; w < NT / 64; ++w) {
     if (w < wave_id()) pre += r[w];
@@ -148,16 +250,12 @@ __device__ __forceinline__ int block_excl_int(int v, unsigned char* red, int* to
 template <int NT>
 __device__ __forceinline__ void block_scan128(hyg_u128 v, hyg_u128* out, unsigned char* red) {
   hyg_u128* r = (hyg_u128*)red;
-  hyg_u128 inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    hyg_u128 n;
-    n.lo = shu(inc.lo, o);
-    n.hi = shu(inc.hi, o);
-    if (lane_id() >= o) inc = hyg_u128_add(inc, n);
-  }
-  __syncthreads();
-  if (lane_id() == 63) r[wave_id()] = inc;
-  __syncthreads();
+  const hyg_u128 inc = wave_incl128(v);
+  hyg_u128 wt;
+  wt.lo = rdlane64(inc.lo, 63); wt.hi = rdlane64(inc.hi, 63);
+  lds_barrier();
+  if (lane_id() == 0) r[wave_id()] = wt;
+  lds_barrier();
   hyg_u128 pre = hyg_u128_zero(), tot = hyg_u128_zero();
   for (int w = 0; w < NT / 64; ++w) {
     if (w < wave_id()) pre = hyg_u128_add(pre, r[w]);
@@ -235,29 +333,34 @@ __device__ __forceinline__ void load_consts(ConstLds& cl, const hyg_tg_consts* _
 // log f_t(next | prev), t >= 1 (case_control_regime_model.py:80-193,
 // case_control_distributions.py:138-151, 246-291); h = hazard of prev.
 // Same branch structure and addition order as oracle/tg_oracle.c:tg_trans.
+__device__ __forceinline__ double tg_trans_sel(double lPm_j, double lpc, double lU1, double lU2, int u, int m,
+                                               int dc, int rc, int dk, int rk, uint64_t next, const Hz4& h);
 __device__ __forceinline__ double tg_trans(const ConstLds& cl, int K, uint64_t prev, uint64_t next, const Hz4& h) {
-  const double NINF = HYG_NINF;
   const int m = hyg_st_m(prev), dc = hyg_st_dc(prev), rc = hyg_st_rc(prev), dk = hyg_st_dk(prev),
             rk = hyg_st_rk(prev);
+  const int m2 = hyg_st_m(next), rc2 = hyg_st_rc(next);
+  return tg_trans_sel(cl.lPm[m * 2 + m2], cl.lPc[rc * K + rc2], cl.lU1, cl.lU2, cl.u, m, dc, rc, dk, rk, next, h);
+}
+
+// The case analysis of tg_trans as selects: every operand is loaded and every
+// candidate sum formed unconditionally (no divergent branches, no loads under
+// a lane condition); the selected value is the same expression, so results
+// are bit-identical.
+__device__ __forceinline__ double tg_trans_sel(double lPm_j, double lpc, double lU1, double lU2, int u, int m,
+                                               int dc, int rc, int dk, int rk, uint64_t next, const Hz4& h) {
+  const double NINF = HYG_NINF;
   const int m2 = hyg_st_m(next), dc2 = hyg_st_dc(next), rc2 = hyg_st_rc(next), dk2 = hyg_st_dk(next),
             rk2 = hyg_st_rk(next);
-  double lm;
-  if ((dk < dc ? dk : dc) >= cl.u) lm = cl.lPm[m * 2 + m2];
-  else lm = (m2 == m) ? 0.0 : NINF;
-  double lc;
-  if (dc2 == 1) lc = h.lrc + cl.lPc[rc * K + rc2];
-  else lc = (dc2 == dc + 1 && rc2 == rc) ? h.l1c : NINF;
-  double lk;
-  if (m2 == 1) {
-    lk = (rk2 == rc2 && dk2 == dc2) ? 0.0 : NINF;
-  } else if (m == 1 && dc2 != 1) {
-    lk = (dk2 == 1 && rk2 != rc2) ? cl.lU1 : NINF;
-  } else if (rc2 == rk && m == 0) {
-    lk = (dk2 == 1 && rk2 != rc2) ? cl.lU1 : NINF;
-  } else {
-    if (dk2 == 1) lk = (rk2 != rc2 && rk2 != rk) ? h.lrk + ((rc2 == rk) ? cl.lU1 : cl.lU2) : NINF;
-    else lk = (dk2 == dk + 1 && rk2 == rk) ? h.l1k : NINF;
-  }
+  const double lm = ((dk < dc ? dk : dc) >= u) ? lPm_j : ((m2 == m) ? 0.0 : NINF);
+  const double lc_cp = h.lrc + lpc;
+  const double lc = (dc2 == 1) ? lc_cp : ((dc2 == dc + 1 && rc2 == rc) ? h.l1c : NINF);
+  const double v1 = (rk2 == rc2 && dk2 == dc2) ? 0.0 : NINF;
+  const double v23 = (dk2 == 1 && rk2 != rc2) ? lU1 : NINF;
+  const double lk_cp = h.lrk + ((rc2 == rk) ? lU1 : lU2);
+  const double v4a = (rk2 != rc2 && rk2 != rk) ? lk_cp : NINF;
+  const double v4b = (dk2 == dk + 1 && rk2 == rk) ? h.l1k : NINF;
+  const double v4 = (dk2 == 1) ? v4a : v4b;
+  const double lk = (m2 == 1) ? v1 : ((m == 1 && dc2 != 1) ? v23 : ((rc2 == rk && m == 0) ? v23 : v4));
   return (lm + lc) + lk;
 }
 
@@ -311,7 +414,9 @@ __device__ __forceinline__ Hz4 child_hz(const ConstLds& cl, int K, uint64_t a, i
   else if (s < 2 * K - 1) { hc = p.c1; hk = cl.hz1[1][hyg_st_rk(x)]; }
   else if (s == 2 * K - 1) {
     if (hyg_st_m(a) == 0) { hc = p.c1; hk = p.kc; }
-    else { hc = hz_at(md, K, 0, hyg_st_rc(x), 0); hk = hz_at(md, K, 1, hyg_st_rk(x), 0); }  // weight is -inf
+    // m = 1: the merge slot's child (1, 0, r, 0, r) has weight -inf, is never
+    // resampled and never becomes an ancestor; its hazards are never used
+    else { hc = cl.hz1[0][hyg_st_rc(x)]; hk = cl.hz1[1][hyg_st_rk(x)]; }
   } else { hc = cl.hz1[0][hyg_st_rc(x)]; hk = cl.hz1[1][hyg_st_rk(x)]; }
   h.lrc = hc.x; h.l1c = hc.y; h.lrk = hk.x; h.l1k = hk.y;
   return h;
@@ -416,14 +521,118 @@ __device__ __forceinline__ double weight_one(const ConstLds& cl, int K, int n, i
   return (pa + lg) - (v < 0.0 ? v : 0.0);
 }
 
+// Scalars of the transition density held in registers by gen_weights.
+struct TransRegs {
+  double lPm0, lPm1, lPm2, lPm3, lU1, lU2;
+  int u;
+};
+
+// tg_trans with the ancestor decoded in registers (same operands, same
+// addition order, so bit-identical); lPc stays in LDS.
+__device__ __forceinline__ double tg_trans_r(const TransRegs& q, const double* __restrict__ lPc, int K, int m,
+                                             int dc, int rc, int dk, int rk, uint64_t next, const Hz4& h) {
+  const int m2 = hyg_st_m(next), rc2 = hyg_st_rc(next);
+  const int j = m * 2 + m2;
+  const double lPm_j = j == 0 ? q.lPm0 : (j == 1 ? q.lPm1 : (j == 2 ? q.lPm2 : q.lPm3));
+  return tg_trans_sel(lPm_j, lPc[rc * K + rc2], q.lU1, q.lU2, q.u, m, dc, rc, dk, rk, next, h);
+}
+
 // All weights of a step t >= 1; returns this thread's max and count of finite weights.
+// With np <= 64 every wave keeps one ancestor per lane in registers and walks
+// the proposal slots s = wave, wave + NT/64, ... (slot-uniform control flow);
+// otherwise one candidate per thread through weight_one.
 template <int NT>
 __device__ __forceinline__ void gen_weights(const ConstLds& cl, int K, int I, int np, int mode, float log_c,
-                                            double lse, const uint64_t* pst, const double* pw, const Hz4* phz,
-                                            const double* Et, double* W, double* m_out, int* c_out) {
+                                            double lse, const uint64_t* __restrict__ pst,
+                                            const double* __restrict__ pw, const Hz4* __restrict__ phz,
+                                            const double* __restrict__ Et, double* __restrict__ W, double* m_out,
+                                            int* c_out) {
   const int N = I * np;
   double m = HYG_NINF;
   int cnt = 0;
+  if (np <= 64) {
+    constexpr int NW = NT / 64;
+    const int lane = lane_id(), wv = wave_id();
+    TransRegs q;
+    q.lPm0 = cl.lPm[0]; q.lPm1 = cl.lPm[1]; q.lPm2 = cl.lPm[2]; q.lPm3 = cl.lPm[3];
+    q.lU1 = cl.lU1; q.lU2 = cl.lU2; q.u = cl.u;
+    const double* __restrict__ lPc = cl.lPc;
+    if (lane < np) {
+      const uint64_t par = pst[lane];
+      const double pa = pw[lane];
+      const Hz4 h = phz[lane];
+      const int am = hyg_st_m(par), adc = hyg_st_dc(par), arc = hyg_st_rc(par), adk = hyg_st_dk(par),
+                ark = hyg_st_rk(par);
+      // w = (base + lg) - sub reproduces the three branches of weight_one exactly
+      double base = pa, sub = 0.0;
+      if (mode == MODE_UNBIASED) base = -cl.log_M + lse;
+      if (mode == MODE_OPTIMAL) {
+        const double v = (double)log_c + (pa - lse);
+        sub = v < 0.0 ? v : 0.0;
+      }
+      // tg_trans of every proposal slot with the child substituted
+      // (case_control_proposal_mappings.py:11-134): the per-ancestor parts
+      // once, per slot only what the slot changes. Same operands and the same
+      // addition order as tg_trans, so the weights are bit-identical.
+      const double NINF = HYG_NINF;
+      const bool ok = (adk < adc ? adk : adc) >= q.u;
+      const int j00 = am * 2;
+      const double lPm_s = j00 == 0 ? q.lPm0 : q.lPm3;  // m' = m
+      const double lm0 = ok ? (am ? q.lPm2 : q.lPm0) : (am == 0 ? 0.0 : NINF);
+      const double lm1 = ok ? (am ? q.lPm3 : q.lPm1) : (am == 1 ? 0.0 : NINF);
+      const double lmA = ok ? lPm_s : 0.0;
+      const double* __restrict__ lPcr = lPc + arc * K;  // row r_c of log P_ctrl
+      const double lcA = (adc + 1 == 1) ? (h.lrc + lPcr[arc]) : h.l1c;  // d_c' = d_c + 1, r_c' = r_c
+      const double lkB = (adk == 0) ? NINF : h.l1k;
+      const double lkA = am == 1 ? ((ark == arc && adk == adc) ? 0.0 : NINF) : (arc == ark ? NINF : lkB);
+      const bool condC = (am == 1 && adc + 1 != 1) || (arc == ark && am == 0);
+      const double lkC_cp = h.lrk + ((arc == ark) ? q.lU1 : q.lU2);
+      const int dD = (am == 0) ? adc + 1 : 0;  // merge slot: both groups at d
+      const double lcD = (dD == 1) ? (h.lrc + lPcr[arc]) : ((dD == adc + 1) ? h.l1c : NINF);
+      const double Ec_rc = Et[arc], Ek_rk = Et[K + ark];
+      auto put = [&](int s, double tr, double e) {
+        double w = NINF;
+        if (hyg_isfinite(tr)) w = (base + (tr + e)) - sub;
+        W[s * np + lane] = w;
+        m = dmax(m, w);
+        cnt += (w > NINF) ? 1 : 0;
+      };
+      const int K2 = 2 * K;
+      for (int s = wv; s < K2; s += NW) {  // slot types A-D (s is wave-uniform)
+        if (s == 0) {
+          put(0, (lmA + lcA) + lkA, Ec_rc + Ek_rk);
+        } else if (s < K) {  // control change to r != r_k
+          const int r = (s - 1 < ark) ? s - 1 : s;
+          put(s, (lm0 + (h.lrc + lPcr[r])) + lkB, Et[r] + Ek_rk);
+        } else if (s < K2 - 1) {  // case change to r != r_c
+          const int qq = s - K;
+          const int r = (qq < arc) ? qq : qq + 1;
+          const double lk = condC ? q.lU1 : ((r != ark) ? lkC_cp : NINF);
+          put(s, (lm0 + lcA) + lk, Ec_rc + Et[K + r]);
+        } else {  // merge
+          put(s, (lm1 + lcD) + 0.0, Ec_rc + Et[K + arc]);
+        }
+      }
+      // two change points (i, j): x = (i == j, 1, i, 1, j)
+      int s = wv;
+      while (s < K2) s += NW;
+      int ii = (s - K2) / K, jj = (s - K2) - ii * K;
+      for (; s < I; s += NW) {
+        const double e = Et[ii] + Et[K + jj];
+        const double lc = h.lrc + lPcr[ii];
+        double lk;
+        if (ii == jj) lk = 0.0;
+        else if (ii == ark && am == 0) lk = q.lU1;
+        else lk = (jj != ark) ? (h.lrk + ((ii == ark) ? q.lU1 : q.lU2)) : NINF;
+        put(s, (((ii == jj) ? lm1 : lm0) + lc) + lk, e);
+        jj += NW;
+        while (jj >= K) { jj -= K; ++ii; }
+      }
+    }
+    *m_out = m;
+    *c_out = cnt;
+    return;
+  }
   for (int n = threadIdx.x; n < N; n += NT) {
     const double w = weight_one(cl, K, n, np, mode, log_c, lse, pst, pw, phz, Et);
     W[n] = w;
@@ -478,7 +687,7 @@ __device__ __forceinline__ void categorical_block(int N, double lmax, LogitFn lo
     if (x >= -70.0) loc = hyg_u128_add(loc, hyg_fix100(hyg_exp(x)));
   }
   block_scan128<NT>(loc, cp, red);
-  __syncthreads();
+  lds_barrier();
   const hyg_u128 total = cp[NT];
   for (int q = threadIdx.x; q < n_draw; q += NT) {
     if (!active(q)) continue;
@@ -540,7 +749,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
   };
   // ---- 1a. bucket histogram
   for (int i = tid; i < kBuckets; i += NT) bcnt[i] = 0;
-  __syncthreads();
+  lds_barrier();
   for (int n = tid; n < N; n += NT) {
     const double w = W[n];
     if (w > HYG_NINF) {
@@ -548,7 +757,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
       if (lw >= thr) atomicAdd(&bcnt[bucket_of(lw)], 1);
     }
   }
-  __syncthreads();
+  lds_barrier();
   SPH(17);
   // ---- 1b. bucket starts (exclusive scan), kBuckets / NT buckets per thread
   {
@@ -566,7 +775,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
     }
     if (tid == 0) sh.n_sig = tot;
   }
-  __syncthreads();
+  lds_barrier();
   SPH(18);
   const int n_sig = sh.n_sig;
   // ---- 1c. scatter into buckets (arbitrary order inside a bucket)
@@ -577,7 +786,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
       if (lw >= thr) keys[atomicAdd(&bpos[bucket_of(lw)], 1)] = sort_key(lw, n);
     }
   }
-  __syncthreads();
+  lds_barrier();
   SPH(19);
   // ---- 1d. rank every key inside its bucket and place it in `sorted` (the
   //          W area: every read of W is done); bpos now holds the bucket ends
@@ -589,7 +798,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
     for (int i = beg; i < end; ++i) rank += (keys[i] < k) ? 1 : 0;
     sorted[beg + rank] = k;
   }
-  __syncthreads();
+  lds_barrier();
   SPH(13);
   // ---- 2. masses and exact prefix sums over contiguous chunks of sorted positions
   const int cs = (n_sig + NT - 1) / NT;
@@ -607,7 +816,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
       pre64[p] = run;
     }
   }
-  __syncthreads();
+  lds_barrier();
   SPH(14);
   // ---- 3. K / log c (loop-variable semantics of :12-31)
   if (wave_id() == 0) {
@@ -639,15 +848,15 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
       // follow a <- max(a, P(c(a))) from a = 0 (the body runs at least once)
       int aa = 0, bb = -1;
       while (aa != bb && aa < N && aa < M) {
-        const int nxt = __shfl(Pa, aa);
+        const int nxt = __builtin_amdgcn_readlane(Pa, aa);
         bb = aa;
         aa = nxt > aa ? nxt : aa;
       }
-      const float lc = __shfl(ca, bb);
+      const float lc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), bb));
       hyg_u192 R;
-      R.w0 = __shfl(rva.w0, bb);
-      R.w1 = __shfl(rva.w1, bb);
-      R.w2 = __shfl(rva.w2, bb);
+      R.w0 = rdlane64(rva.w0, bb);
+      R.w1 = rdlane64(rva.w1, bb);
+      R.w2 = rdlane64(rva.w2, bb);
       if (lane == 0) {
         sh.Kk = bb;
         sh.log_c = lc;
@@ -698,7 +907,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   SPH(15);
   int Kk = sh.Kk;
   const float log_c = sh.log_c;
@@ -713,7 +922,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
     parents[Kk + j] = key_index(sorted[Kk]);  // unfilled -> residual index 0
   }
   for (int p = tid; p < Kk; p += NT) parents[p] = key_index(sorted[p]);
-  __syncthreads();
+  lds_barrier();
   if (p0 < n_sig && p0 + cs > Kk && L > 0) {
     // first target not reached before this chunk: #{j : tau_j <= C(p0 - 1)}
     int j = 0;
@@ -826,7 +1035,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     StepScalars* s0 = (StepScalars*)rec0;
     s0->mode = MODE_INIT; s0->n_par = 0; s0->log_c = 0.0f; s0->r_ph = sh.r_ph; s0->lse = 0.0; s0->pad = 0.0;
   }
-  __syncthreads();
+  lds_barrier();
   double mloc;
   int cloc;
   gen_weights_init<NT>(cl, K, sh.r_ph, erow(ering, 0, K2), W, &mloc, &cloc);
@@ -847,7 +1056,18 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       break;  // uniform
     }
     // ---- log_softmax / reduce_logsumexp of the weights of step t-1
-    const double logS = log_mass_sum<NT>(W, N, mx, red);
+    double logS;
+    {
+      hyg_u128 sacc = hyg_u128_zero();
+      for (int n = tid; n < N; n += NT) {
+        const double x = W[n] - mx;
+        if (x >= -70.0) sacc = hyg_u128_add(sacc, hyg_fix100(hyg_exp(x)));
+      }
+      PH(12);
+      const hyg_u128 S = block_sum128<NT>(sacc, red);
+      PH(11);
+      logS = hyg_log(hyg_u128_to_f64(S, 100));
+    }
     const double lse = logS + mx;
     PH(1);
     int mode, np;
@@ -864,7 +1084,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       v.lo = (uint64_t)loc;
       v.hi = 0;
       block_scan128<NT>(v, cp128, red);
-      __syncthreads();
+      lds_barrier();
       int o = (int)cp128[tid].lo;
       for (int n = p0; n < p1; ++n)
         if (W[n] > HYG_NINF) parents[o++] = n;
@@ -886,14 +1106,14 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         mode = MODE_UNBIASED;
         log_c = 0.0f;
         const double lmax = (double)key_value(((const uint64_t*)W)[0]);
-        __syncthreads();  // the sorted keys in the W area are replaced by the regenerated weights
+        lds_barrier();  // the sorted keys in the W area are replaced by the regenerated weights
         if (prev_mode == MODE_INIT) {
           gen_weights_init<NT>(cl, K, sh.r_ph, erow(ering, t - 1, K2), W, &mloc, &cloc);
         } else {
           gen_weights<NT>(cl, K, I, np_prev, prev_mode, prev_logc, prev_lse, pst, pw, phz, erow(ering, t - 1, K2),
                           W, &mloc, &cloc);
         }
-        __syncthreads();
+        lds_barrier();
         auto logit = [&](int n) -> double {
           const double w = W[n];
           return (w > HYG_NINF) ? (double)(float)((w - mx) - logS) : HYG_NINF;
@@ -903,13 +1123,13 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         };
         auto out = [&](int q, int n) { parents[q] = n; };
         auto all = [](int) { return true; };
-        __syncthreads();
+        lds_barrier();
         categorical_block<NT>(N, lmax, logit, M, all, rnd, out, cp128, red);
       } else {
         mode = MODE_OPTIMAL;
       }
     }
-    __syncthreads();
+    lds_barrier();
     PH(4);
     // ---- gather the ancestors (state, weight, own hazards), record them,
     //      and start the hazard-row prefetch for their children
@@ -974,17 +1194,18 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     prev_mode = mode;
     prev_logc = log_c;
     prev_lse = lse;
-    __syncthreads();  // every read of the previous ancestors is done
+    lds_barrier();  // every read of the previous ancestors is done
     if (have_pf) {
       pst[tid] = gs;
       pw[tid] = gw;
       phz[tid] = gh;
     }
-    __syncthreads();
+    lds_barrier();
     PH(5);
     // ---- propose and weight the particles of step t
     gen_weights<NT>(cl, K, I, np, mode, log_c, lse, pst, pw, phz,
                     erow(ering, t, K2), W, &mloc, &cloc);
+    PH(7);
     N = I * np;
     if (have_pf) pf[tid] = pfa;
     if (eload) {
@@ -995,6 +1216,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         if (i < e_tot) dst[i] = ebuf[q];
       }
     }
+    PH(8);
     block_max_cnt<NT>(mloc, cloc, red, &mx, &cnt);
     PH(6);
   }
@@ -1085,7 +1307,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     load_eblock(ering, Ech, bi, T, K2, NT);
     if (bi > 0) load_eblock(ering, Ech, bi - 1, T, K2, NT);
   }
-  __syncthreads();
+  lds_barrier();
 
   for (int t = T - 1; t >= 0; --t) {
     // ---- regenerate the particles of step t from its record (in LDS)
@@ -1140,7 +1362,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         ebuf[q] = (i < e_tot) ? Ech[(size_t)t0 * K2 + i] : 0.0;
       }
     }
-    __syncthreads();
+    lds_barrier();
     auto state_of = [&](int n) -> uint64_t {
       if (s.mode == MODE_INIT) return init_state(K, n);
       const int sl = fdiv(n, np, rnp);
@@ -1159,14 +1381,14 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     if (t == T - 1) {
       // ---- B draws from the final weights (:383-385)
       const double lmax = block_max<NT>(mloc, red);
-      if (!(lmax > HYG_NINF)) { if (tid == 0) sh.status = HYG_ENUMERIC; __syncthreads(); break; }
+      if (!(lmax > HYG_NINF)) { if (tid == 0) sh.status = HYG_ENUMERIC; lds_barrier(); break; }
       auto logit = [&](int n) -> double { return W[n]; };
       auto rnd = [&](int q) -> uint64_t {
         return hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)q);
       };
       auto out = [&](int q, int n) { idx[q] = n; };
       auto all = [](int) { return true; };
-      __syncthreads();
+      lds_barrier();
       categorical_block<NT>(N, lmax, logit, B, all, rnd, out, cp128, red);
     } else {
       // ---- backward-kernel rows (:400-435), one per distinct next state
@@ -1198,7 +1420,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         }
         sh.ng = ng;
       }
-      __syncthreads();
+      lds_barrier();
       const int ng = sh.ng;
       bool fail = false;
       for (int g = 0; g < ng; ++g) {
@@ -1224,11 +1446,11 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         };
         auto out = [&](int b, int n) { idx[b] = n; };
         categorical_block<NT>(N, lmax, logit, B, in_g, rnd, out, cp128, red);
-        __syncthreads();
+        lds_barrier();
       }
-      if (fail) { if (tid == 0) sh.status = HYG_ENUMERIC; __syncthreads(); break; }
+      if (fail) { if (tid == 0) sh.status = HYG_ENUMERIC; lds_barrier(); break; }
     }
-    __syncthreads();
+    lds_barrier();
     // ---- trajectories and test-function means at t (run_inference_two_groups.py:233-240, 294-314)
     for (int b = tid; b < B; b += NT) {
       const uint64_t x = state_of(idx[b]);
@@ -1241,7 +1463,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
     }
     // ---- record t-1 (+ hazard rows) replaces record t once every read of it is done
-    __syncthreads();
+    lds_barrier();
     if (have1) {
       pst[tid] = st1;
       pw[tid] = w1;
@@ -1258,7 +1480,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         if (i < e_tot) dst[i] = ebuf[q];
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < 2 * K + 1) {
       int cntv = 0;
       for (int b = 0; b < B; ++b) {
@@ -1276,7 +1498,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     w1 = w2;
     s1 = s2;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid == 0 && status_out) status_out[blockIdx.x] = sh.status;
 }
 
@@ -1370,14 +1592,15 @@ static int launch_chains_nt(const ModelDev& md, const hyg_tg_consts& c, const Ch
       for (int k = 0; k < 24; ++k) tot[k] += h[(size_t)i * 24 + k];
     const double steps = (double)tot[23];
     fprintf(stderr, "[hyg phases NT=%d] chains=%d steps=%.0f cycles/step:", NT, n_chains, steps);
-    const char* nm[7] = {"top", "lse", "compact", "resample", "fallback", "gather", "weights"};
+    const char* nm[9] = {"top", "lse", "compact", "resample", "fallback", "gather", "wmax", "wgen", "wstore"};
     double sum = 0;
-    for (int k = 0; k < 7; ++k) {
+    for (int k = 0; k < 9; ++k) {
       fprintf(stderr, " %s=%.0f", nm[k], tot[k] / steps);
       sum += tot[k] / steps;
     }
     fprintf(stderr, " total=%.0f | keep_steps=%.0f mean_nsig=%.1f mean_n2=%.1f", sum, (double)tot[10],
-            tot[9] / (steps - tot[10]), tot[11] / (steps - tot[10]));
+            tot[9] / (steps - tot[10]), 0.0);
+    fprintf(stderr, " | lse loop=%.0f lse reduce=%.0f", tot[12] / steps, tot[11] / steps);
     const double opt = steps - tot[10];
     fprintf(stderr, " | per optimal step: hist=%.0f bscan=%.0f scatter=%.0f bsort=%.0f scan=%.0f kloop=%.0f systematic=%.0f\n",
             tot[17] / opt, tot[18] / opt, tot[19] / opt, tot[13] / opt, tot[14] / opt, tot[15] / opt, tot[16] / opt);
