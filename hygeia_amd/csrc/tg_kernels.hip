@@ -503,12 +503,11 @@ __device__ __forceinline__ const double* erow(const double* ering, int t, int K2
   return ering + ((size_t)((t / kEBlock) & 1) * kEBlock + (t % kEBlock)) * K2;
 }
 
-// Weight of particle n of a step t >= 1 from the ancestors (pst, pw, phz) and
-// the step scalars (_filter_one_step :235-270).
-__device__ __forceinline__ double weight_one(const ConstLds& cl, int K, int n, int np, int mode, float log_c,
-                                             double lse, const uint64_t* pst, const double* pw, const Hz4* phz,
-                                             const double* Et) {
-  const int s = fdiv(n, np, 1.0f / (float)np), a = n - s * np;
+// Weight of the child in slot s of ancestor a at a step t >= 1, from the
+// ancestors (pst, pw, phz) and the step scalars (_filter_one_step :235-270).
+__device__ __forceinline__ double weight_at(const ConstLds& cl, int K, int a, int s, int mode, float log_c,
+                                            double lse, const uint64_t* pst, const double* pw, const Hz4* phz,
+                                            const double* Et) {
   const uint64_t par = pst[a];
   const uint64_t x = tg_xi(K, par, s);
   const double tr = tg_trans(cl, K, par, x, phz[a]);
@@ -519,6 +518,13 @@ __device__ __forceinline__ double weight_one(const ConstLds& cl, int K, int n, i
   if (mode == MODE_UNBIASED) return (-cl.log_M + lse) + lg;
   const double v = (double)log_c + (pa - lse);
   return (pa + lg) - (v < 0.0 ? v : 0.0);
+}
+// Weight of particle n = s * np + a.
+__device__ __forceinline__ double weight_one(const ConstLds& cl, int K, int n, int np, int mode, float log_c,
+                                             double lse, const uint64_t* pst, const double* pw, const Hz4* phz,
+                                             const double* Et) {
+  const int s = fdiv(n, np, 1.0f / (float)np), a = n - s * np;
+  return weight_at(cl, K, a, s, mode, log_c, lse, pst, pw, phz, Et);
 }
 
 // Scalars of the transition density held in registers by gen_weights.
@@ -750,6 +756,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
   // ---- 1a. bucket histogram
   for (int i = tid; i < kBuckets; i += NT) bcnt[i] = 0;
   lds_barrier();
+  #pragma unroll 4
   for (int n = tid; n < N; n += NT) {
     const double w = W[n];
     if (w > HYG_NINF) {
@@ -779,6 +786,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
   SPH(18);
   const int n_sig = sh.n_sig;
   // ---- 1c. scatter into buckets (arbitrary order inside a bucket)
+  #pragma unroll 4
   for (int n = tid; n < N; n += NT) {
     const double w = W[n];
     if (w > HYG_NINF) {
@@ -795,6 +803,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
     const int q = bucket_of(key_value(k));
     const int end = bpos[q], beg = end - bcnt[q];
     int rank = 0;
+#pragma unroll 4
     for (int i = beg; i < end; ++i) rank += (keys[i] < k) ? 1 : 0;
     sorted[beg + rank] = k;
   }
@@ -1059,10 +1068,10 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     double logS;
     {
       hyg_u128 sacc = hyg_u128_zero();
-      for (int n = tid; n < N; n += NT) {
-        const double x = W[n] - mx;
-        if (x >= -70.0) sacc = hyg_u128_add(sacc, hyg_fix100(hyg_exp(x)));
-      }
+      // branch-free body (fix100(exp(x)) is 0 for every x < -70, so the
+      // oracle's skip needs no test here), unrolled for ILP
+#pragma unroll 4
+      for (int n = tid; n < N; n += NT) sacc = hyg_u128_add(sacc, hyg_fix100(hyg_exp(W[n] - mx)));
       PH(12);
       const hyg_u128 S = block_sum128<NT>(sacc, red);
       PH(11);
@@ -1240,12 +1249,62 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
 #undef PH
 }
 
+// ------------------------------------------------- backward-kernel rows
+// Child of an ancestor (registers) in proposal slot s (wave-uniform), with the
+// child's own hazard rows, exactly as tg_xi + child_hz produce them.
+struct Child {
+  int m, dc, rc, dk, rk;
+  Hz4 h;
+};
+__device__ __forceinline__ Child child_of(const ConstLds& cl, int K, int am, int adc, int arc, int adk, int ark,
+                                          const Pf3& p, int s) {
+  Child x;
+  double2 hc, hk;
+  if (s == 0) {
+    x.m = am; x.dc = adc + 1; x.rc = arc; x.dk = adk + 1; x.rk = ark;
+    hc = p.c1; hk = p.k1;
+  } else if (s < K) {
+    const int r = (s - 1 < ark) ? s - 1 : s;
+    x.m = 0; x.dc = 1; x.rc = r; x.dk = adk + 1; x.rk = ark;
+    hc = cl.hz1[0][r]; hk = p.k1;
+  } else if (s < 2 * K - 1) {
+    const int qq = s - K;
+    const int r = (qq < arc) ? qq : qq + 1;
+    x.m = 0; x.dc = adc + 1; x.rc = arc; x.dk = 1; x.rk = r;
+    hc = p.c1; hk = cl.hz1[1][r];
+  } else if (s == 2 * K - 1) {
+    const int d = (am == 0) ? adc + 1 : 0;
+    x.m = 1; x.dc = d; x.rc = arc; x.dk = d; x.rk = arc;
+    if (am == 0) { hc = p.c1; hk = p.kc; }
+    else { hc = cl.hz1[0][arc]; hk = cl.hz1[1][arc]; }
+  } else {
+    const int j = s - 2 * K, i = j / K, jj = j - i * K;
+    x.m = (i == jj); x.dc = 1; x.rc = i; x.dk = 1; x.rk = jj;
+    hc = cl.hz1[0][i]; hk = cl.hz1[1][jj];
+  }
+  x.h.lrc = hc.x; x.h.l1c = hc.y; x.h.lrk = hk.x; x.h.l1k = hk.y;
+  return x;
+}
+// false when tg_trans(x -> next) selects a constant -inf branch whatever the
+// table values (the selected value is then -inf; true leaves it to the values)
+__device__ __forceinline__ bool trans_possible(int u, const Child& x, int mn, int dcn, int rcn, int dkn, int rkn) {
+  const bool lm = ((x.dk < x.dc ? x.dk : x.dc) >= u) || (mn == x.m);
+  const bool lc = (dcn == 1) || (dcn == x.dc + 1 && rcn == x.rc);
+  bool lk;
+  if (mn == 1) lk = (rkn == rcn && dkn == dcn);
+  else if (x.m == 1 && dcn != 1) lk = (dkn == 1 && rkn != rcn);
+  else if (rcn == x.rk && x.m == 0) lk = (dkn == 1 && rkn != rcn);
+  else lk = (dkn == 1) ? (rkn != rcn && rkn != x.rk) : (dkn == x.dk + 1 && rkn == x.rk);
+  return lm && lc && lk;
+}
+
 template <int NT>
 __global__ void __launch_bounds__(NT)
 tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                    const uint8_t* __restrict__ ws, const int32_t* status_in, int16_t* __restrict__ o_merged,
                    int16_t* __restrict__ o_control, int16_t* __restrict__ o_case, float* __restrict__ o_split,
-                   float* __restrict__ o_regime, int32_t* status_out, Lay lay) {
+                   float* __restrict__ o_regime, int32_t* status_out, Lay lay,
+                   unsigned long long* __restrict__ dbg) {
   const hyg_tg_consts* __restrict__ c = md.consts;
   const int K = c->K, M = c->M, B = c->B, I = c->I, K2 = 2 * K, tid = threadIdx.x;
   const ChainDev ch = chains[blockIdx.x];
@@ -1273,6 +1332,14 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   const double* Ech = E + ch.site_begin * K2;
   load_consts(cl, c, md);
   if (tid == 0) sh.status = HYG_OK;
+  unsigned long long* ph_acc = sh.ph;
+  if (tid < 24) ph_acc[tid] = 0;
+#define BPH(k)                                                     \
+  if (dbg && tid == 0) {                                           \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    ph_acc[k] += now_ - ph_acc[23];                                \
+    ph_acc[23] = now_;                                             \
+  }
   // Records are read ahead in two stages: step t consumes record t from LDS,
   // stores record t-1 (read during step t+1) with its hazard rows (issued at
   // the top of step t), and issues the read of record t-2.
@@ -1308,6 +1375,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     if (bi > 0) load_eblock(ering, Ech, bi - 1, T, K2, NT);
   }
   lds_barrier();
+  if (dbg && tid == 0) ph_acc[23] = __builtin_amdgcn_s_memtime();
 
   for (int t = T - 1; t >= 0; --t) {
     // ---- regenerate the particles of step t from its record (in LDS)
@@ -1317,16 +1385,21 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     const Hz4* PHZ = phz;
     const Pf3* PF = pf;
     const float rnp = (np > 0) ? 1.0f / (float)np : 0.0f;
-    int N;
-    double mloc;
-    int cloc;
-    if (s.mode == MODE_INIT) {
-      gen_weights_init<NT>(cl, K, s.r_ph, Et, W, &mloc, &cloc);
-      N = K * K;
-    } else {
-      gen_weights<NT>(cl, K, I, np, s.mode, s.log_c, s.lse, P, pw, PHZ, Et, W, &mloc, &cloc);
-      N = I * np;
-    }
+    const int N = (s.mode == MODE_INIT) ? K * K : I * np;
+    double mloc = HYG_NINF;
+    int cloc = 0;
+    // The rows of the backward kernel need the weights of the few candidates
+    // that can reach a trajectory's next state only; all N weights are built
+    // for the final step's draw and for the general paths.
+    const bool fast = (s.mode != MODE_INIT) && np <= 64 && B <= 64 && c->Nmax >= 192 && t != T - 1;
+    bool w_ready = false;
+    auto make_W = [&]() {
+      if (s.mode == MODE_INIT) gen_weights_init<NT>(cl, K, s.r_ph, Et, W, &mloc, &cloc);
+      else gen_weights<NT>(cl, K, I, np, s.mode, s.log_c, s.lse, P, pw, PHZ, Et, W, &mloc, &cloc);
+      w_ready = true;
+    };
+    if (!fast) make_W();
+    BPH(0);
     // ---- hazard rows of record t-1's ancestors (arrived: read during step t+1)
     double2 h1c = make_double2(0.0, 0.0), h1k = make_double2(0.0, 0.0);
     Pf3 pf1;
@@ -1363,6 +1436,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       }
     }
     lds_barrier();
+    BPH(1);
     auto state_of = [&](int n) -> uint64_t {
       if (s.mode == MODE_INIT) return init_state(K, n);
       const int sl = fdiv(n, np, rnp);
@@ -1422,31 +1496,149 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       }
       lds_barrier();
       const int ng = sh.ng;
+      if (dbg && tid == 0) ph_acc[10] += ng;
+      BPH(2);
       bool fail = false;
       for (int g = 0; g < ng; ++g) {
         const uint64_t xn = gst[g];
-        double m = HYG_NINF;
-        for (int n = tid; n < N; n += NT) {
-          const double w = W[n];
-          double l = HYG_NINF;
-          if (w > HYG_NINF) {
-            const uint64_t x = state_of(n);
-            const double f = tg_trans(cl, K, x, xn, hz_of_n(n));
-            if (hyg_isfinite(f)) l = f + w;
+        const int mn = hyg_st_m(xn), dcn = hyg_st_dc(xn), rcn = hyg_st_rc(xn), dkn = hyg_st_dk(xn),
+                  rkn = hyg_st_rk(xn);
+        // ---- finite logits l_n = log f(xn | x_n) + W_n, gathered into a short
+        //      list (n, l_n): only a few dozen of the N candidates can reach xn
+        if (tid == 0) sh.cnt = 0;
+        lds_barrier();
+        int* lst_n = (int*)cp128;  // list indices (cp area, NT+1 u128 = 4(NT+1) ints)
+        double* lst_l = Lg;        // list logits
+        const int cap = (4 * (NT + 1) < c->Nmax) ? 4 * (NT + 1) : c->Nmax;
+        if (!fast) {
+          for (int n = tid; n < N; n += NT) {
+            const double w = W[n];
+            double l = HYG_NINF;
+            if (w > HYG_NINF) {
+              const double f = tg_trans(cl, K, state_of(n), xn, hz_of_n(n));
+              if (hyg_isfinite(f)) l = f + w;
+            }
+            if (l > HYG_NINF) {
+              const int pos = atomicAdd(&sh.cnt, 1);
+              if (pos < cap) { lst_n[pos] = n; lst_l[pos] = l; }
+            }
           }
-          Lg[n] = l;
-          m = dmax(m, l);
+        } else {
+          constexpr int NW = NT / 64;
+          const int lane = lane_id(), wv = wave_id();
+          const bool act = lane < np;
+          const uint64_t par = act ? P[lane] : 0;
+          const int am = hyg_st_m(par), adc = hyg_st_dc(par), arc = hyg_st_rc(par), adk = hyg_st_dk(par),
+                    ark = hyg_st_rk(par);
+          Pf3 pa{};
+          if (act) pa = PF[lane];
+          // Only slots whose child can have d_c = dcn - 1 (or a control change
+          // point when dcn = 1) can reach xn: lc of tg_trans is a constant -inf
+          // otherwise (ancestors always have d_c >= 1).
+          int r0a, r0b, r1a, r1b;
+          if (dcn >= 3) { r0a = 0; r0b = 1; r1a = K; r1b = 2 * K; }                         // A, C, D
+          else if (dcn == 2) { r0a = 1; r0b = K; r1a = 2 * K + rcn * K; r1b = r1a + K; }   // B, E(i = rcn)
+          else { r0a = 0; r0b = I; r1a = I; r1b = I; }
+          for (int part = 0; part < 2; ++part) {
+            const int sa = part ? r1a : r0a, sb = part ? r1b : r0b;
+            for (int sl = sa + wv; sl < sb; sl += NW) {
+              const Child x = child_of(cl, K, am, adc, arc, adk, ark, pa, sl);
+              const bool poss = act && trans_possible(cl.u, x, mn, dcn, rcn, dkn, rkn);
+              if (__ballot(poss) == 0) continue;  // nothing in this slot reaches xn
+              double l = HYG_NINF;
+              if (poss) {
+                const double w = weight_at(cl, K, lane, sl, s.mode, s.log_c, s.lse, P, pw, PHZ, Et);
+                if (w > HYG_NINF) {
+                  const double f = tg_trans_sel(cl.lPm[x.m * 2 + mn], cl.lPc[x.rc * K + rcn], cl.lU1, cl.lU2,
+                                                cl.u, x.m, x.dc, x.rc, x.dk, x.rk, xn, x.h);
+                  if (hyg_isfinite(f)) l = f + w;
+                }
+              }
+              const unsigned long long mask = __ballot(l > HYG_NINF);
+              if (mask) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&sh.cnt, __popcll(mask));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (l > HYG_NINF) {
+                  const int pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                  if (pos < cap) { lst_n[pos] = sl * np + lane; lst_l[pos] = l; }
+                }
+              }
+            }
+          }
         }
-        const double lmax = block_max<NT>(m, red);
-        if (!(lmax > HYG_NINF)) { fail = true; break; }  // uniform
-        auto logit = [&](int n) -> double { return Lg[n]; };
-        auto in_g = [&](int b) { return grp[b] == g; };
+        lds_barrier();
+        BPH(3);
+        const int L = sh.cnt;
+        if (dbg && tid == 0) ph_acc[11] += L;
+        if (L == 0) { fail = true; break; }  // uniform: every logit -inf
         auto rnd = [&](int b) -> uint64_t {
           return hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
         };
-        auto out = [&](int b, int n) { idx[b] = n; };
-        categorical_block<NT>(N, lmax, logit, B, in_g, rnd, out, cp128, red);
+        if (L <= 64 && B <= 64 && c->Nmax >= 192) {
+          // ---- one wave: order the list by n, exact masses, scan, draws
+          if (wave_id() == 0) {
+            const int lane = lane_id();
+            const bool v = lane < L;
+            const int myn = v ? lst_n[lane] : 0x7fffffff;
+            const double myl = v ? lst_l[lane] : HYG_NINF;
+            int rank = 0;
+#pragma unroll 4
+            for (int j = 0; j < L; ++j) rank += (lst_n[j] < myn) ? 1 : 0;  // broadcast reads
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+            if (v) { lst_n[rank] = myn; lst_l[rank] = myl; }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+            const int sn = v ? lst_n[lane] : 0;
+            const double sv = v ? lst_l[lane] : HYG_NINF;
+            const double lmax = wave_max(sv);
+            hyg_u128 ms = hyg_u128_zero();
+            if (v) ms = hyg_fix100(hyg_exp(sv - lmax));
+            const hyg_u128 cdf = wave_incl128(ms);
+            hyg_u128 total;
+            total.lo = rdlane64(cdf.lo, L - 1);
+            total.hi = rdlane64(cdf.hi, L - 1);
+            hyg_u128* cdfa = (hyg_u128*)(Lg + 64);  // behind the 64 list logits
+            if (v) cdfa[lane] = cdf;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+            // lane b draws for trajectory b: first list entry with cdf > target
+            if (lane < B && grp[lane] == g) {
+              const hyg_u128 tb = hyg_scale_target(rnd(lane), total);
+              int lo = 0, hi = L - 1;
+              while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (hyg_u128_lt(tb, cdfa[mid])) hi = mid; else lo = mid + 1;
+              }
+              idx[lane] = lst_n[lo];
+            }
+          }
+          BPH(4);
+        } else {
+          // ---- general case: logits of all N in index order, block categorical
+          if (!w_ready) {
+            lds_barrier();  // the list areas are reused below
+            make_W();
+            lds_barrier();
+          }
+          double m = HYG_NINF;
+          for (int n = tid; n < N; n += NT) {
+            const double w = W[n];
+            double l = HYG_NINF;
+            if (w > HYG_NINF) {
+              const double f = tg_trans(cl, K, state_of(n), xn, hz_of_n(n));
+              if (hyg_isfinite(f)) l = f + w;
+            }
+            Lg[n] = l;
+            m = dmax(m, l);
+          }
+          const double lmax = block_max<NT>(m, red);
+          auto logit = [&](int n) -> double { return Lg[n]; };
+          auto in_g = [&](int b) { return grp[b] == g; };
+          auto out = [&](int b, int n) { idx[b] = n; };
+          categorical_block<NT>(N, lmax, logit, B, in_g, rnd, out, cp128, red);
+        }
         lds_barrier();
+        BPH(5);
       }
       if (fail) { if (tid == 0) sh.status = HYG_ENUMERIC; lds_barrier(); break; }
     }
@@ -1462,6 +1654,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
       o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
     }
+    BPH(6);
     // ---- record t-1 (+ hazard rows) replaces record t once every read of it is done
     lds_barrier();
     if (have1) {
@@ -1500,6 +1693,11 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   }
   lds_barrier();
   if (tid == 0 && status_out) status_out[blockIdx.x] = sh.status;
+  if (dbg && tid == 0) {
+    for (int k = 0; k < 23; ++k) dbg[(size_t)blockIdx.x * 24 + k] = ph_acc[k];
+    dbg[(size_t)blockIdx.x * 24 + 23] = (unsigned long long)T;
+  }
+#undef BPH
 }
 
 // -------------------------------------------------------------- launchers
@@ -1605,11 +1803,33 @@ static int launch_chains_nt(const ModelDev& md, const hyg_tg_consts& c, const Ch
     fprintf(stderr, " | per optimal step: hist=%.0f bscan=%.0f scatter=%.0f bsort=%.0f scan=%.0f kloop=%.0f systematic=%.0f\n",
             tot[17] / opt, tot[18] / opt, tot[19] / opt, tot[13] / opt, tot[14] / opt, tot[15] / opt, tot[16] / opt);
   }
+  unsigned long long* dbgb = nullptr;
+  if (want_dbg) (void)hipMalloc((void**)&dbgb, sizeof(unsigned long long) * 24 * n_chains);
+  if (dbgb) (void)hipMemsetAsync(dbgb, 0, sizeof(unsigned long long) * 24 * n_chains, s);
   ev_record(2, false, s);
   hipLaunchKernelGGL(tg_backward_kernel<NT>, dim3(n_chains), dim3(NT), lb.total, s, md, chains_dev, E,
                      (const uint8_t*)ws, (const int32_t*)out.status, out.merged, out.control, out.kase,
-                     out.split_probs, out.regime_probs, out.status, lb);
+                     out.split_probs, out.regime_probs, out.status, lb, dbgb);
   ev_record(2, true, s);
+  if (dbgb) {
+    std::vector<unsigned long long> h((size_t)24 * n_chains);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), dbgb, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
+    (void)hipFree(dbgb);
+    unsigned long long tot[24] = {0};
+    for (int i = 0; i < n_chains; ++i)
+      for (int k = 0; k < 24; ++k) tot[k] += h[(size_t)i * 24 + k];
+    const double steps = (double)tot[23];
+    const char* nm[7] = {"gen", "issue", "dedupe", "list", "wave0", "tail", "traj"};
+    fprintf(stderr, "[hyg backward phases NT=%d] cycles/step:", NT);
+    double sum = 0;
+    for (int k = 0; k < 7; ++k) {
+      fprintf(stderr, " %s=%.0f", nm[k], tot[k] / steps);
+      sum += tot[k] / steps;
+    }
+    fprintf(stderr, " total(+tail)=%.0f | groups/step=%.2f finite logits/group=%.1f\n", sum, tot[10] / steps,
+            (double)(tot[11] & 0xffffffffull) / (tot[10] > 0 ? (double)tot[10] : 1.0));
+  }
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }
 

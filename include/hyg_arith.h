@@ -39,10 +39,14 @@
 #if defined(__HIPCC__)
 #define HYG_HD __host__ __device__ __forceinline__
 #define HYG_FLOOR(x) __builtin_floor(x)
+#define HYG_FMIN(a, b) __builtin_fmin(a, b)
+#define HYG_FMAX(a, b) __builtin_fmax(a, b)
 #else
 #include <math.h>
 #define HYG_HD static inline
 #define HYG_FLOOR(x) floor(x)
+#define HYG_FMIN(a, b) fmin(a, b)
+#define HYG_FMAX(a, b) fmax(a, b)
 #endif
 
 /* ------------------------------------------------------------------ bits */
@@ -68,74 +72,85 @@ HYG_HD double hyg_pow2(int e) { return hyg_bits_f64((uint64_t)(e + 1023) << 52);
 #define HYG_LN2_LO 1.90821492927058770002e-10
 #define HYG_INV_LN2 1.44269504088896338700e+00
 
-/* exp(x) for double x. Range reduction x = k ln2 + r, |r| <= ln2/2, then the
- * degree-13 Taylor polynomial of e^r by Horner (remainder < 4e-18), then an
- * exact (or single-rounding, for subnormal results) scale by 2^k. */
+/* exp(x) for double x. Range reduction x = k ln2 + r, |r| <= ln2/2, the
+ * degree-13 Taylor polynomial of e^r (remainder < 4e-18) evaluated by
+ * Estrin's scheme (dependency depth 8 instead of Horner's 26: the GPU
+ * kernels are latency-bound on these chains), then an exact (or
+ * single-rounding, for subnormal results) scale by 2^k. Written without
+ * branches: special inputs are resolved by selects at the end. */
 HYG_HD double hyg_exp(double x) {
-  if (x != x) return x;
-  if (x > 709.782712893383973096) return HYG_INF;
-  if (x < -745.13321910194110842) return 0.0;
-  const double kd = HYG_FLOOR(x * HYG_INV_LN2 + 0.5);
+  const double xc = HYG_FMIN(HYG_FMAX(x, -746.0), 710.0); /* NaN -> -746 (result selected below) */
+  const double kd = HYG_FLOOR(xc * HYG_INV_LN2 + 0.5);
   const int k = (int)kd;
-  const double hi = x - kd * HYG_LN2_HI;
+  const double hi = xc - kd * HYG_LN2_HI;
   const double lo = kd * HYG_LN2_LO;
   const double r = hi - lo;
-  double p = 1.6059043836821614599e-10;  /* 1/13! */
-  p = 2.0876756987868098979e-09 + r * p; /* 1/12! */
-  p = 2.5052108385441718775e-08 + r * p; /* 1/11! */
-  p = 2.7557319223985890653e-07 + r * p; /* 1/10! */
-  p = 2.7557319223985890653e-06 + r * p; /* 1/9! */
-  p = 2.4801587301587301566e-05 + r * p; /* 1/8! */
-  p = 1.9841269841269841253e-04 + r * p; /* 1/7! */
-  p = 1.3888888888888888889e-03 + r * p; /* 1/6! */
-  p = 8.3333333333333332177e-03 + r * p; /* 1/5! */
-  p = 4.1666666666666664354e-02 + r * p; /* 1/4! */
-  p = 1.6666666666666665741e-01 + r * p; /* 1/3! */
-  p = 0.5 + r * p;
-  p = 1.0 + r * p;
-  p = 1.0 + r * p;
-  if (k > 1023) return (p * 2.0) * hyg_pow2(k - 1);
-  if (k >= -1021) return p * hyg_pow2(k);
-  /* subnormal result: exact scale into the normal range, then one rounding */
-  return (p * hyg_pow2(k + 54)) * hyg_pow2(-54);
+  const double r2 = r * r;
+  const double r4 = r2 * r2;
+  const double r8 = r4 * r4;
+  const double q0 = 1.0 + 1.0 * r;
+  const double q1 = 0.5 + 1.6666666666666665741e-01 * r;                   /* 1/2!, 1/3! */
+  const double q2 = 4.1666666666666664354e-02 + 8.3333333333333332177e-03 * r; /* 1/4!, 1/5! */
+  const double q3 = 1.3888888888888888889e-03 + 1.9841269841269841253e-04 * r; /* 1/6!, 1/7! */
+  const double q4 = 2.4801587301587301566e-05 + 2.7557319223985890653e-06 * r; /* 1/8!, 1/9! */
+  const double q5 = 2.7557319223985890653e-07 + 2.5052108385441718775e-08 * r; /* 1/10!, 1/11! */
+  const double q6 = 2.0876756987868098979e-09 + 1.6059043836821614599e-10 * r; /* 1/12!, 1/13! */
+  const double s0 = q0 + q1 * r2;
+  const double s1 = q2 + q3 * r2;
+  const double s2 = q4 + q5 * r2;
+  const double u0 = s0 + s1 * r4;
+  const double u1 = s2 + q6 * r4;
+  const double p = u0 + u1 * r8;
+  /* k > 1023: (p*2) 2^(k-1); k >= -1021: p 2^k; else (p 2^(k+54)) 2^-54 */
+  const int big = k > 1023, sub = k < -1021;
+  const int k1 = big ? k - 1 : (sub ? k + 54 : k);
+  const double p1 = big ? p * 2.0 : p;
+  double v = p1 * hyg_pow2(k1);
+  v = sub ? v * 5.5511151231257827021e-17 : v; /* 2^-54 */
+  v = (x < -745.13321910194110842) ? 0.0 : v;
+  v = (x > 709.782712893383973096) ? HYG_INF : v;
+  return (x != x) ? x : v;
 }
 
 /* log(x) for double x: x = 2^e m, m in (sqrt(1/2), sqrt(2)], f = m - 1,
  * s = f/(2+f), log(1+f) = f - (f^2/2 - s (f^2/2 + R(s^2))) with the atanh
- * series R(z) = sum_{i>=1} 2 z^i/(2i+1) to i = 11 (|s| <= 0.1716). */
+ * series R(z) = sum_{i>=1} 2 z^i/(2i+1) to i = 11 (|s| <= 0.1716), the
+ * polynomial by Estrin's scheme. Branch-free like hyg_exp. */
 HYG_HD double hyg_log(double x) {
-  if (x != x || x < 0.0) return HYG_NAN;
-  if (x == 0.0) return HYG_NINF;
   uint64_t b = hyg_f64_bits(x);
-  if ((b >> 52) == 0x7ff) return x; /* +inf */
-  int e = 0;
-  if ((b >> 52) == 0) { /* subnormal */
-    x = x * 18014398509481984.0; /* 2^54 */
-    b = hyg_f64_bits(x);
-    e = -54;
-  }
-  e += (int)((b >> 52) & 0x7ff) - 1023;
+  const int subn = (b >> 52) == 0; /* zero or subnormal */
+  const double xs = subn ? x * 18014398509481984.0 : x; /* 2^54 */
+  b = hyg_f64_bits(xs);
+  int e = (subn ? -54 : 0) + (int)((b >> 52) & 0x7ff) - 1023;
   double m = hyg_bits_f64((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-  if (m > 1.41421356237309504880) { m = m * 0.5; e += 1; }
+  const int hi_m = m > 1.41421356237309504880;
+  m = hi_m ? m * 0.5 : m;
+  e += hi_m;
   const double f = m - 1.0;
   const double s = f / (2.0 + f);
   const double z = s * s;
-  double R = 0.08695652173913043478; /* 2/23 */
-  R = 0.09523809523809523810 + z * R; /* 2/21 */
-  R = 0.10526315789473684211 + z * R; /* 2/19 */
-  R = 0.11764705882352941176 + z * R; /* 2/17 */
-  R = 0.13333333333333333333 + z * R; /* 2/15 */
-  R = 0.15384615384615384615 + z * R; /* 2/13 */
-  R = 0.18181818181818181818 + z * R; /* 2/11 */
-  R = 0.22222222222222222222 + z * R; /* 2/9 */
-  R = 0.28571428571428571429 + z * R; /* 2/7 */
-  R = 0.40000000000000000000 + z * R; /* 2/5 */
-  R = 0.66666666666666666667 + z * R; /* 2/3 */
-  R = z * R;
+  const double z2 = z * z;
+  const double z4 = z2 * z2;
+  const double z8 = z4 * z4;
+  /* R/z = sum_{i=0}^{10} a_i z^i, a_i = 2/(2i+3) */
+  const double a01 = 0.66666666666666666667 + 0.40000000000000000000 * z;
+  const double a23 = 0.28571428571428571429 + 0.22222222222222222222 * z;
+  const double a45 = 0.18181818181818181818 + 0.15384615384615384615 * z;
+  const double a67 = 0.13333333333333333333 + 0.11764705882352941176 * z;
+  const double a89 = 0.10526315789473684211 + 0.09523809523809523810 * z;
+  const double a10 = 0.08695652173913043478;
+  const double b0 = a01 + a23 * z2;
+  const double b1 = a45 + a67 * z2;
+  const double b2 = a89 + a10 * z2;
+  const double c0 = b0 + b1 * z4;
+  const double R = z * (c0 + b2 * z8);
   const double hfsq = 0.5 * f * f;
   const double l1p = f - (hfsq - s * (hfsq + R));
   const double ed = (double)e;
-  return ed * HYG_LN2_HI + (ed * HYG_LN2_LO + l1p);
+  double v = ed * HYG_LN2_HI + (ed * HYG_LN2_LO + l1p);
+  v = ((b >> 52) == 0x7ff) ? xs : v; /* +inf */
+  v = (x == 0.0) ? HYG_NINF : v;
+  return (x != x || x < 0.0) ? HYG_NAN : v;
 }
 
 /* f32 versions used where the reference computes in float32
@@ -163,19 +178,23 @@ HYG_HD hyg_u128 hyg_u128_add(hyg_u128 a, hyg_u128 b) {
 HYG_HD int hyg_u128_lt(hyg_u128 a, hyg_u128 b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
 HYG_HD int hyg_u128_is_zero(hyg_u128 a) { return (a.lo | a.hi) == 0; }
 
-/* floor(e * 2^100) for e in [0, 1]; masses below 2^-100 become 0. */
+/* floor(e * 2^100) for e in [0, 1]; masses below 2^-100 become 0.
+ * Branch-free (selects only), so unrolled GPU loops can interleave. */
 HYG_HD hyg_u128 hyg_fix100(double e) {
-  hyg_u128 r = hyg_u128_zero();
-  if (!(e > 0.0)) return r;
   const uint64_t b = hyg_f64_bits(e);
   const int E = (int)((b >> 52) & 0x7ff);
-  if (E == 0) return r;
   const uint64_t mant = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
-  const int sh = E - 975; /* value*2^100 = mant * 2^(E-1075+100) */
-  if (sh >= 64) { r.hi = mant << (sh - 64); }
-  else if (sh > 0) { r.lo = mant << sh; r.hi = mant >> (64 - sh); }
-  else if (sh == 0) { r.lo = mant; }
-  else if (sh > -64) { r.lo = mant >> (-sh); }
+  const int sh = E - 975; /* value*2^100 = mant * 2^(E-1075+100); sh <= 48 for e <= 1 */
+  const int shp = (sh > 0 ? sh : 0) & 63, shn = (sh < 0 ? -sh : 0) & 63;
+  const uint64_t up_lo = mant << shp;
+  const uint64_t up_hi = (mant >> 1) >> (63 - shp); /* mant >> (64 - shp), 0 for shp = 0 */
+  const uint64_t dn_lo = mant >> shn;
+  hyg_u128 r;
+  r.lo = (sh >= 0) ? up_lo : ((sh > -64) ? dn_lo : 0);
+  r.hi = (sh > 0) ? up_hi : 0;
+  const int zero = !(e > 0.0) || E == 0 || sh >= 64;
+  r.lo = zero ? 0 : r.lo;
+  r.hi = zero ? 0 : r.hi;
   return r;
 }
 
@@ -227,24 +246,23 @@ HYG_HD int hyg_u192_is_zero(hyg_u192 a) { return (a.w0 | a.w1 | a.w2) == 0; }
 
 /* exact integer image of an f32 mass m in [0, 1]: m * 2^149. */
 HYG_HD hyg_u192 hyg_fix149f(float m) {
-  hyg_u192 r = hyg_u192_zero();
+  /* branch-free: the 24-bit significand shifted left by E - 1 (0..126) */
   const uint32_t b = hyg_f32_bits(m);
-  if (b == 0 || (b >> 31)) return r;
   const int E = (int)((b >> 23) & 0xff);
   const uint64_t man = b & 0x7fffffu;
-  if (E == 0) { r.w0 = man; return r; }
-  const uint64_t v = man | 0x800000u;
-  const int sh = E - 1; /* 0..126 for m <= 1 */
-  if (sh < 64) {
-    r.w0 = v << sh;
-    r.w1 = sh ? (v >> (64 - sh)) : 0;
-  } else if (sh < 128) {
-    const int s2 = sh - 64;
-    r.w1 = v << s2;
-    r.w2 = s2 ? (v >> (64 - s2)) : 0;
-  } else {
-    r.w2 = v << (sh - 128);
-  }
+  const uint64_t v = (E == 0) ? man : (man | 0x800000u);
+  const int sh = (E == 0) ? 0 : E - 1;
+  const int s0 = sh & 63;
+  const uint64_t lo = v << s0;
+  const uint64_t hi = (v >> 1) >> (63 - s0); /* v >> (64 - s0), 0 for s0 = 0 */
+  hyg_u192 r;
+  r.w0 = (sh < 64) ? lo : 0;
+  r.w1 = (sh < 64) ? hi : ((sh < 128) ? lo : 0);
+  r.w2 = (sh < 64) ? 0 : ((sh < 128) ? hi : lo);
+  const int zero = (b == 0) || (b >> 31);
+  r.w0 = zero ? 0 : r.w0;
+  r.w1 = zero ? 0 : r.w1;
+  r.w2 = zero ? 0 : r.w2;
   return r;
 }
 

@@ -20,6 +20,7 @@ import math
 import numpy as np
 
 NINF = float("-inf")
+STEP_HOOK = None
 M64 = (1 << 64) - 1
 
 # ------------------------------------------------------------ arithmetic
@@ -41,6 +42,7 @@ def _pow2(e: int) -> float:
 
 
 def det_exp(x: float) -> float:
+    """hyg_exp: Taylor degree 13 by Estrin's scheme (same operations, same order)."""
     if x != x:
         return x
     if x > 709.782712893383973096:
@@ -52,9 +54,20 @@ def det_exp(x: float) -> float:
     hi = x - kd * _LN2_HI
     lo = kd * _LN2_LO
     r = hi - lo
-    p = _EXP_C[0]
-    for c in _EXP_C[1:]:
-        p = c + r * p
+    r2 = r * r
+    r4 = r2 * r2
+    r8 = r4 * r4
+    c = [1.0, 1.0, 0.5, 1.6666666666666665741e-01, 4.1666666666666664354e-02, 8.3333333333333332177e-03,
+         1.3888888888888888889e-03, 1.9841269841269841253e-04, 2.4801587301587301566e-05,
+         2.7557319223985890653e-06, 2.7557319223985890653e-07, 2.5052108385441718775e-08,
+         2.0876756987868098979e-09, 1.6059043836821614599e-10]
+    q = [c[2 * i] + c[2 * i + 1] * r for i in range(7)]
+    s0 = q[0] + q[1] * r2
+    s1 = q[2] + q[3] * r2
+    s2 = q[4] + q[5] * r2
+    u0 = s0 + s1 * r4
+    u1 = s2 + q[6] * r4
+    p = u0 + u1 * r8
     if k > 1023:
         return (p * 2.0) * _pow2(k - 1)
     if k >= -1021:
@@ -63,6 +76,7 @@ def det_exp(x: float) -> float:
 
 
 def det_log(x: float) -> float:
+    """hyg_log: atanh series by Estrin's scheme (same operations, same order)."""
     if x != x or x < 0.0:
         return math.nan
     if x == 0.0:
@@ -78,10 +92,23 @@ def det_log(x: float) -> float:
     f = m - 1.0
     s = f / (2.0 + f)
     z = s * s
-    R = _LOG_C[0]
-    for c in _LOG_C[1:]:
-        R = c + z * R
-    R = z * R
+    z2 = z * z
+    z4 = z2 * z2
+    z8 = z4 * z4
+    a = [0.66666666666666666667, 0.40000000000000000000, 0.28571428571428571429, 0.22222222222222222222,
+         0.18181818181818181818, 0.15384615384615384615, 0.13333333333333333333, 0.11764705882352941176,
+         0.10526315789473684211, 0.09523809523809523810]
+    a01 = a[0] + a[1] * z
+    a23 = a[2] + a[3] * z
+    a45 = a[4] + a[5] * z
+    a67 = a[6] + a[7] * z
+    a89 = a[8] + a[9] * z
+    a10 = 0.08695652173913043478
+    b0 = a01 + a23 * z2
+    b1 = a45 + a67 * z2
+    b2 = a89 + a10 * z2
+    c0 = b0 + b1 * z4
+    R = z * (c0 + b2 * z8)
     hfsq = 0.5 * f * f
     l1p = f - (hfsq - s * (hfsq + R))
     ed = float(e)
@@ -319,6 +346,8 @@ def run_chain(model: Model, E: np.ndarray, seed: int, chain: int):
             rec["mode"] = "keep"
         else:
             lw32 = [np.float32((w - mx) - logS) for w in W]
+            if STEP_HOOK is not None:  # diagnostics (tools/), not part of the algorithm
+                STEP_HOOK(t, lw32)
             keys = sorted(_sort_key(lw32[n], n) for n in range(N))
             order = [k & 0xFFFFFFFF for k in keys]
             mass = [det_expf(lw32[n]) for n in order]
