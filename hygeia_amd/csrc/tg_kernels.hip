@@ -422,11 +422,41 @@ __device__ __forceinline__ Hz4 child_hz(const ConstLds& cl, int K, uint64_t a, i
   return h;
 }
 
+// tg_xi + child_hz without divergent branches (slot s varies per lane in
+// the gather): every slot type's child is formed and the right one selected.
+__device__ __forceinline__ uint64_t tg_xi_hz_sel(const ConstLds& cl, int K, float rK, uint64_t a, int s,
+                                                 const Pf3& p, Hz4* hout) {
+  const int m = hyg_st_m(a), dc = hyg_st_dc(a), rc = hyg_st_rc(a), dk = hyg_st_dk(a), rk = hyg_st_rk(a);
+  const int rB = (s - 1 < rk) ? s - 1 : s;
+  const int qq = s - K, rC = (qq < rc) ? qq : qq + 1;
+  const int dD = (m == 0) ? dc + 1 : 0;
+  const int j = s - 2 * K;
+  int i = (int)((float)(j > 0 ? j : 0) * rK);
+  if (i * K > j) --i;
+  if ((i + 1) * K <= j) ++i;
+  const int jj = j - i * K;
+  const bool tA = s == 0, tB = s < K, tC = s < 2 * K - 1, tD = s == 2 * K - 1;
+  int xm, xdc, xrc, xdk, xrk;
+  if (tA) { xm = m; xdc = dc + 1; xrc = rc; xdk = dk + 1; xrk = rk; }
+  else if (tB) { xm = 0; xdc = 1; xrc = rB; xdk = dk + 1; xrk = rk; }
+  else if (tC) { xm = 0; xdc = dc + 1; xrc = rc; xdk = 1; xrk = rC; }
+  else if (tD) { xm = 1; xdc = dD; xrc = rc; xdk = dD; xrk = rc; }
+  else { xm = (i == jj); xdc = 1; xrc = i; xdk = 1; xrk = jj; }
+  // hazard rows: prefetched rows where the duration continues, d = 1 rows at a change
+  const bool c_cont = tA || (!tB && tC) || (tD && m == 0);
+  const bool k_cont = tA || (tB && !tA);
+  const double2 hc = c_cont ? p.c1 : cl.hz1[0][xrc];
+  const double2 hk = (tD && m == 0) ? p.kc : (k_cont ? p.k1 : cl.hz1[1][xrk]);
+  hout->lrc = hc.x; hout->l1c = hc.y; hout->lrk = hk.x; hout->l1k = hk.y;
+  return hyg_st_pack(xm, xdc, xrc, xdk, xrk);
+}
+
 // ------------------------------------------------------------ LDS layout
 struct Shared {  // broadcast scalars of one workgroup
   double mx, logS;
   float c_new, log_c;
   int cnt, n_sig, Kk, status, r_ph, ng;
+  float Unext;  // systematic-resampling uniform of the next step, drawn during the gather
   unsigned sig_ctr;
   hyg_u192 R, preK;
   unsigned long long ph[24];
@@ -738,7 +768,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
                                  uint64_t* keys, int* bcnt, int* bpos, hyg_u192* pre64, hyg_u192* tau, int* parents,
                                  Shared& sh,
                                  const ConstLds& cl, unsigned char* red, int M, int cnt_fin, uint64_t seed,
-                                 uint64_t chain_id, int t, unsigned long long* ph, bool timed) {
+                                 uint64_t chain_id, int t, float Usys, unsigned long long* ph, bool timed) {
   const int tid = threadIdx.x;
 #define SPH(k)                                                     \
   if (timed && tid == 0) {                                         \
@@ -814,14 +844,39 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
   const int p0 = tid * cs;
   const int p1 = (p0 + cs < n_sig) ? p0 + cs : n_sig;
   hyg_u192 loc = hyg_u192_zero();
-  for (int p = p0; p < p1; ++p) loc = hyg_u192_add(loc, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
+  // the f32 masses of this thread's chunk stay in registers for the prefix,
+  // the K search and the systematic walk (chunks longer than kMR recompute)
+  constexpr int kMR = 8;
+  float mreg[kMR];
+  const bool inreg = cs <= kMR;
+  if (inreg) {
+#pragma unroll
+    for (int i = 0; i < kMR; ++i) {
+      const int p = p0 + i;
+      mreg[i] = 0.0f;
+      if (p < p1) mreg[i] = hyg_expf(key_value(sorted[p]));
+    }
+#pragma unroll
+    for (int i = 0; i < kMR; ++i) loc = hyg_u192_add(loc, hyg_fix149f(mreg[i]));
+  } else {
+    for (int p = p0; p < p1; ++p) loc = hyg_u192_add(loc, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
+  }
+  auto mass_at = [&](int p) -> float {  // mass of sorted position p of this thread's chunk
+    if (inreg) {
+      float v = 0.0f;
+#pragma unroll
+      for (int i = 0; i < kMR; ++i) v = (p - p0 == i) ? mreg[i] : v;
+      return v;
+    }
+    return hyg_expf(key_value(sorted[p]));
+  };
   hyg_u192 total;
   const hyg_u192 myex = block_excl192<NT>(loc, red, &total);
   const int npre = M < 64 ? M : 64;  // pre64 holds min(M, 64) entries (make_layout)
   if (p0 < npre) {  // inclusive prefix of the first npre sorted positions
     hyg_u192 run = myex;
     for (int p = p0; p < p1 && p < npre; ++p) {
-      run = hyg_u192_add(run, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
+      run = hyg_u192_add(run, hyg_fix149f(mass_at(p)));
       pre64[p] = run;
     }
   }
@@ -923,7 +978,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
   if (Kk >= N || !hyg_isfinitef(log_c)) return;  // caller runs the unbiased fallback
   // ---- 4. deterministic top-K, systematic residual with exact thresholds
   const int L = M - Kk;
-  const float U = hyg_u01f(hyg_rand64(seed, chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)t, 0));
+  const float U = Usys;  // hyg_u01f(hyg_rand64(seed, chain_id, HYG_RNG_SYSTEMATIC, t, 0)), drawn ahead
   const float Lf = (float)L;
   const hyg_u192 R = sh.R, preK = sh.preK;
   for (int j = tid; j < L; j += NT) {
@@ -945,7 +1000,7 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
     }
     hyg_u192 C = myex;
     for (int p = p0; p < p1 && j < L; ++p) {
-      C = hyg_u192_add(C, hyg_fix149f(hyg_expf(key_value(sorted[p]))));
+      C = hyg_u192_add(C, hyg_fix149f(mass_at(p)));
       if (p >= Kk) {
         while (j < L && hyg_u192_ge(C, tau[j])) {
           parents[Kk + j] = key_index(sorted[p]);
@@ -1039,6 +1094,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
   load_eblock(ering, Ech, 0, T, K2, NT);
   load_eblock(ering, Ech, 1, T, K2, NT);
   if (tid == 0) {
+    sh.Unext = hyg_u01f(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_SYSTEMATIC, 1, 0));
     sh.r_ph = (int)hyg_mulhi64(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_PHANTOM, 0, 0), (uint64_t)K);
     sh.status = HYG_OK;
     StepScalars* s0 = (StepScalars*)rec0;
@@ -1064,6 +1120,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       if (tid == 0) sh.status = HYG_ENUMERIC;
       break;  // uniform
     }
+    const float Ucur = sh.Unext;  // written during step t-1's gather, before two barriers
     // ---- log_softmax / reduce_logsumexp of the weights of step t-1
     double logS;
     {
@@ -1103,7 +1160,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       // ---- OptimalFiniteState (resampling_functions.py:7-52)
       PH(2);
       optimal_resample<NT>(W, (uint64_t*)W, N, mx, logS, c->sig_thresh, keys, bcnt, bpos, pre64, tau, parents, sh,
-                           cl, red, M, cnt, ch.seed, ch.chain_id, t, ph_acc, dbg != nullptr);
+                           cl, red, M, cnt, ch.seed, ch.chain_id, t, Ucur, ph_acc, dbg != nullptr);
       if (dbg && tid == 0) ph_acc[9] += sh.n_sig;
       PH(3);
       int Kk = sh.Kk;
@@ -1159,21 +1216,34 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         s = init_state(K, n);
         const double2 hc = cl.hz1[0][hyg_st_rc(s)], hk = cl.hz1[1][hyg_st_rk(s)];
         h.lrc = hc.x; h.l1c = hc.y; h.lrk = hk.x; h.l1k = hk.y;
-      } else {
-        const int sl = fdiv(n, np_prev, 1.0f / (float)np_prev);
-        const int ao = n - sl * np_prev;
-        const uint64_t anc = pst[ao];
-        s = tg_xi(K, anc, sl);
-        h = child_hz(cl, K, anc, sl, pf[ao], md);
       }
-      // the weight of candidate n of step t-1, recomputed (the W area may hold the sort)
+      // the weight of candidate n of step t-1, recomputed (the W area may hold
+      // the sort): weight_at's arithmetic with the child formed once
       double w;
       if (prev_mode == MODE_INIT) {
         const int i = n / K, j = n - (n / K) * K;
         const double* E0 = erow(ering, 0, K2);
         w = (E0[i] + E0[K + j]) + ((i == j) ? cl.lPc[sh.r_ph * K + i] : HYG_NINF);
       } else {
-        w = weight_one(cl, K, n, np_prev, prev_mode, prev_logc, prev_lse, pst, pw, phz, erow(ering, t - 1, K2));
+        const int sl = fdiv(n, np_prev, 1.0f / (float)np_prev);
+        const int ao = n - sl * np_prev;
+        const uint64_t anc = pst[ao];
+        const Pf3 pfo = pf[ao];
+        const Hz4 hzo = phz[ao];
+        const double pao = pw[ao];
+        s = tg_xi_hz_sel(cl, K, 1.0f / (float)K, anc, sl, pfo, &h);
+        const double tr = tg_trans(cl, K, anc, s, hzo);
+        const double* Ep = erow(ering, t - 1, K2);
+        w = HYG_NINF;
+        if (hyg_isfinite(tr)) {
+          const double lg = tr + (Ep[hyg_st_rc(s)] + Ep[K + hyg_st_rk(s)]);
+          if (prev_mode == MODE_KEEP) w = pao + lg;
+          else if (prev_mode == MODE_UNBIASED) w = (-cl.log_M + prev_lse) + lg;
+          else {
+            const double v = (double)prev_logc + (pao - prev_lse);
+            w = (pao + lg) - (v < 0.0 ? v : 0.0);
+          }
+        }
       }
       gs = s;
       gw = w;
@@ -1184,6 +1254,10 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     }
     if (tid == 0) {
       rs->mode = mode; rs->n_par = np; rs->log_c = log_c; rs->r_ph = 0; rs->lse = lse; rs->pad = 0.0;
+    }
+    if (wave_id() == NT / 64 - 1) {  // a wave with no ancestor (when NT > M): next step's uniform
+      const float un = hyg_u01f(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)(t + 1), 0));
+      if (lane_id() == 0) sh.Unext = un;
     }
     // emission block prefetch (registers), stored into the ring after the weights
     constexpr int EQ = (kEBlock * 2 * HYG_KMAX + NT - 1) / NT;  // rows of one block per thread
@@ -1589,7 +1663,6 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
             if (v) { lst_n[rank] = myn; lst_l[rank] = myl; }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
-            const int sn = v ? lst_n[lane] : 0;
             const double sv = v ? lst_l[lane] : HYG_NINF;
             const double lmax = wave_max(sv);
             hyg_u128 ms = hyg_u128_zero();
