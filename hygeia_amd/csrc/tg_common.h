@@ -9,7 +9,8 @@
 
 namespace hyg {
 
-constexpr int kDefaultThreads = 256;  // threads of the per-chain workgroup (HYG_THREADS overrides)
+constexpr int kDefaultThreads = 256;     // forward workgroup size
+constexpr int kDefaultThreadsBwd = 256;  // backward workgroup size (HYG_THREADS[_FWD/_BWD] override)
 constexpr int kEBlock = 8;     // emission rows staged in LDS per block of steps
 
 // Device-side chain descriptor (lives in the workspace header).

@@ -1787,13 +1787,17 @@ void ev_record(int k, bool end, hipStream_t s) {
   (void)hipEventRecord(e, s);
   g_ev_used[k] = true;
 }
-int threads_per_chain() {
-  static int nt = [] {
-    const char* v = getenv("HYG_THREADS");
-    const int x = v ? atoi(v) : kDefaultThreads;
-    return (x == 64 || x == 128 || x == 256 || x == 512) ? x : kDefaultThreads;
-  }();
-  return nt;
+// Threads per chain workgroup (HYG_THREADS, or HYG_THREADS_FWD / _BWD per kernel).
+int threads_per_chain(bool backward) {
+  static int nt[2] = {0, 0};
+  const int k = backward ? 1 : 0;
+  if (!nt[k]) {
+    const char* v = getenv(backward ? "HYG_THREADS_BWD" : "HYG_THREADS_FWD");
+    if (!v) v = getenv("HYG_THREADS");
+    const int x = v ? atoi(v) : (backward ? kDefaultThreadsBwd : kDefaultThreads);
+    nt[k] = (x == 64 || x == 128 || x == 256 || x == 512) ? x : kDefaultThreads;
+  }
+  return nt[k];
 }
 }  // namespace
 
@@ -1812,10 +1816,10 @@ int last_kernel_ms(float* out3) {
 }
 
 size_t forward_lds_bytes(const hyg_tg_consts& c) {
-  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(), false).total;
+  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(false), false).total;
 }
 size_t backward_lds_bytes(const hyg_tg_consts& c) {
-  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(), true).total;
+  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(true), true).total;
 }
 
 int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* meth_c, const uint16_t* tot_c,
@@ -1832,17 +1836,13 @@ int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* 
 }
 
 template <int NT>
-static int launch_chains_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
+static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
                             const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
   const Lay lf = make_layout(c.K, c.M, c.B, c.Nmax, NT, false);
-  const Lay lb = make_layout(c.K, c.M, c.B, c.Nmax, NT, true);
-  if (lf.total > 160 * 1024 || lb.total > 160 * 1024) return HYG_EUNSUPPORTED;
+  if (lf.total > 160 * 1024) return HYG_EUNSUPPORTED;
   if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
   if (hipFuncSetAttribute((const void*)tg_forward_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lf.total) != hipSuccess)
-    return HYG_EDEVICE;
-  if (hipFuncSetAttribute((const void*)tg_backward_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lb.total) != hipSuccess)
     return HYG_EDEVICE;
   unsigned long long* dbg = nullptr;
   static const bool want_dbg = getenv("HYG_DEBUG_PHASES") != nullptr;
@@ -1876,6 +1876,19 @@ static int launch_chains_nt(const ModelDev& md, const hyg_tg_consts& c, const Ch
     fprintf(stderr, " | per optimal step: hist=%.0f bscan=%.0f scatter=%.0f bsort=%.0f scan=%.0f kloop=%.0f systematic=%.0f\n",
             tot[17] / opt, tot[18] / opt, tot[19] / opt, tot[13] / opt, tot[14] / opt, tot[15] / opt, tot[16] / opt);
   }
+  return HYG_OK;
+}
+
+template <int NT>
+static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
+                              const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
+  const Lay lb = make_layout(c.K, c.M, c.B, c.Nmax, NT, true);
+  if (lb.total > 160 * 1024) return HYG_EUNSUPPORTED;
+  if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
+  if (hipFuncSetAttribute((const void*)tg_backward_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lb.total) != hipSuccess)
+    return HYG_EDEVICE;
+  static const bool want_dbg = getenv("HYG_DEBUG_PHASES") != nullptr;
   unsigned long long* dbgb = nullptr;
   if (want_dbg) (void)hipMalloc((void**)&dbgb, sizeof(unsigned long long) * 24 * n_chains);
   if (dbgb) (void)hipMemsetAsync(dbgb, 0, sizeof(unsigned long long) * 24 * n_chains, s);
@@ -1910,11 +1923,19 @@ int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* ch
                   const double* E, uint8_t* ws, const hyg_tg_outputs& out, void* stream) {
   if (n_chains <= 0) return HYG_OK;
   hipStream_t s = (hipStream_t)stream;
-  switch (threads_per_chain()) {
-    case 64: return launch_chains_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s);
-    case 128: return launch_chains_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s);
-    case 256: return launch_chains_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s);
-    default: return launch_chains_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s);
+  int rc;
+  switch (threads_per_chain(false)) {
+    case 64: rc = launch_forward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s); break;
+    case 128: rc = launch_forward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s); break;
+    case 256: rc = launch_forward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s); break;
+    default: rc = launch_forward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s); break;
+  }
+  if (rc != HYG_OK) return rc;
+  switch (threads_per_chain(true)) {
+    case 64: return launch_backward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s);
+    case 128: return launch_backward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s);
+    case 256: return launch_backward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s);
+    default: return launch_backward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s);
   }
 }
 
