@@ -82,6 +82,14 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so) next to
+    # the system one this library links. Both work in one process only when
+    # torch's is initialised first, so torch is imported before our runtime
+    # can initialise (it is the device-memory / stream plumbing anyway).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         from . import build as _build
         _build.build()

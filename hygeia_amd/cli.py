@@ -1,0 +1,290 @@
+"""`hygeia infer` on the MI355X path: a drop-in for src/two_group/run_inference_two_groups.py.
+
+Same flags (absl spellings and defaults, run_inference_two_groups.py:19-72), same
+input files (B.1 of SURVEY.md: whole-chromosome gzip CSVs in --data_dir and
+theta_{chrom}.csv.gz in --single_group_dir), same segment slicing and exit
+behaviour (:194-218), same output directory and files (:101-108, 246-322):
+
+    results_dir/chrom_{chrom}_{batch}/
+        flags{seed}.txt
+        observations_{control,case}.csv.gz, n_total_reads_{control,case}.csv.gz, positions.csv.gz
+        optimal_backward_particles_{merged,control,case}_state_{N}_{seed}.npz   (int16, trimmed)
+        optimal_split_probs_{N}_{seed}.npz, optimal_regime_probs_{N}_{seed}.npz (float32, untrimmed)
+        log_normalizing_constants_optimal_{seed}.txt, optimal_time_{seed}.txt,
+        optimal_time_backward_{seed}.txt
+
+so modules/two_group/4_infer.nf runs it unchanged (through bin/hygeia). The
+filter and the backward simulation run in the HIP kernels behind the C ABI
+(include/hygeia_amd.h); there is no CPU path.
+
+The random streams are Philox4x64-10 keyed by (seed, chain id) with
+chain id = crc32(chrom) << 32 | batch, so a (chrom, batch, seed) task gives the
+same trajectories here, in a batched multi-chain run, and on any GPU count.
+"""
+from __future__ import annotations
+
+import gzip
+import math
+import os
+import sys
+import time
+import zlib
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+# (name, kind, default, help) in the reference's definition order (:19-72)
+FLAGS_SPEC = [
+    ("mu", "list", "0.95,0.05,0.80,0.20,0.50,0.50", "mu of the beta distribution"),
+    ("sigma", "list", "0.05,0.05,0.1,0.1,0.1,0.2886751", "sigma of the beta distribution"),
+    ("minimum_duration", "int", 3, "minimum duration between change points"),
+    ("omega_case", "float", 0.8, "omega parameter for duration of case group"),
+    ("merge_log_prob", "float", math.log(0.1), "value for merge probability"),
+    ("split_prob", "float", 0.01, "value for split probability"),
+    ("num_resampled_particles", "multi_int", [50], "number M of particles that are resampled"),
+    ("num_samples_backward", "int", 25, "number of particles used for backward sampling"),
+    ("multinomial", "bool", False, "multinomial or residual resampling"),
+    ("chrom", "string", "22", "The chromosome to analyze"),
+    ("results_dir", "string", os.path.join(os.path.dirname(os.getcwd()), "test"), "Directory for the results"),
+    ("data_dir", "string", "data", "Directory of the read data"),
+    ("single_group_dir", "string", os.path.join("test_data", "single_group_results"),
+     "Directory of the single group estimation results"),
+    ("seed", "int", 0, "seed used for sampling random variables"),
+    ("batch", "int", 0, "index of the selected chromosome segment"),
+    ("segment_size", "int", 100000, "size of the selected chromosome segment (in CpG sites)"),
+    ("buffer_size", "int", 5000, "size of the buffer segment (in CpG sites)"),
+]
+
+
+class FlagError(ValueError):
+    pass
+
+
+def parse_flags(argv: Sequence[str]) -> Dict[str, object]:
+    """absl-style parsing: --name=value, --name value, --bool / --nobool, list
+    flags comma separated, multi flags repeated."""
+    spec = {n: (k, d) for n, k, d, _ in FLAGS_SPEC}
+    out: Dict[str, object] = {}
+    multi: Dict[str, List[int]] = {}
+    i = 0
+    argv = list(argv)
+    while i < len(argv):
+        a = argv[i]
+        if a == "--":
+            break
+        if not a.startswith("-"):
+            raise FlagError(f"unexpected argument {a!r}")
+        body = a.lstrip("-")
+        name, eq, val = body.partition("=")
+        if name not in spec and name.startswith("no") and name[2:] in spec and spec[name[2:]][0] == "bool":
+            if eq:
+                raise FlagError(f"--{name} takes no value")
+            out[name[2:]] = False
+            i += 1
+            continue
+        if name not in spec:
+            raise FlagError(f"Unknown command line flag '{name}'")
+        kind = spec[name][0]
+        if kind == "bool":
+            if eq:
+                v = val.lower()
+                if v not in ("true", "false", "1", "0"):
+                    raise FlagError(f"invalid boolean value for --{name}: {val}")
+                out[name] = v in ("true", "1")
+            else:
+                out[name] = True
+            i += 1
+            continue
+        if not eq:
+            if i + 1 >= len(argv):
+                raise FlagError(f"Flag --{name} must have a value other than None.")
+            val = argv[i + 1]
+            i += 2
+        else:
+            i += 1
+        try:
+            if kind == "int":
+                out[name] = int(val)
+            elif kind == "float":
+                out[name] = float(val)
+            elif kind == "list":
+                out[name] = [x for x in val.split(",") if x != ""]
+            elif kind == "multi_int":
+                multi.setdefault(name, []).extend(int(x) for x in val.split(","))
+            else:
+                out[name] = val
+        except ValueError as e:
+            raise FlagError(f"invalid value for --{name}: {val!r} ({e})")
+    for n, v in multi.items():
+        out[n] = v
+    for n, (k, d) in spec.items():
+        if n not in out:
+            out[n] = d.split(",") if k == "list" else d
+    return out
+
+
+def serialize_flags(f: Dict[str, object]) -> str:
+    """The flags file content (absl FlagValues serialisation, definition order)."""
+    lines = []
+    for n, k, _, _ in FLAGS_SPEC:
+        v = f[n]
+        if k == "bool":
+            lines.append(f"--{n}" if v else f"--no{n}")
+        elif k == "list":
+            lines.append(f"--{n}={','.join(v)}")
+        elif k == "multi_int":
+            lines.extend(f"--{n}={x}" for x in v)
+        else:
+            lines.append(f"--{n}={v}")
+    return "\n".join(lines)
+
+
+def chain_id(chrom: str, batch: int) -> int:
+    return (zlib.crc32(str(chrom).encode()) << 32) | (int(batch) & 0xFFFFFFFF)
+
+
+def _read_matrix(path: str) -> np.ndarray:
+    import pandas as pd
+
+    return pd.read_csv(path, sep=",", header=None, dtype=np.float64).to_numpy()
+
+
+def read_theta(single_group_dir: str, chrom: str) -> np.ndarray:
+    """theta_{chrom}.csv.gz, column 'data' (run_inference_two_groups.py:76-79)."""
+    import pandas as pd
+
+    df = pd.read_table(os.path.join(single_group_dir, f"theta_{chrom}.csv.gz"), sep=",")
+    return pd.to_numeric(df["data"]).to_numpy(dtype=np.float64)
+
+
+def segment_index(n_sites: int, batch: int, segment_size: int, buffer_size: int):
+    """Rows of the batch (run_inference_two_groups.py:194-218): (slice, return range) or None."""
+    if batch * segment_size > n_sites:
+        return None
+    lo = max(0, batch * segment_size - buffer_size)
+    hi = min((batch + 1) * segment_size + buffer_size, n_sites)
+    T = hi - lo
+    if batch == 0:
+        ret = (0, min(T, segment_size))
+    else:
+        ret = (buffer_size, min(T, buffer_size + segment_size))
+    return (lo, hi), ret
+
+
+def _savetxt(path: str, a: np.ndarray) -> None:
+    np.savetxt(path, a, delimiter=",")  # default fmt '%.18e', gzip by extension, as the reference
+
+
+def infer(argv: Sequence[str]) -> int:
+    f = parse_flags(argv)
+    seed, chrom, batch = int(f["seed"]), str(f["chrom"]), int(f["batch"])
+    s = serialize_flags(f)
+    print("specified flags:\n{}".format(s))
+    path = os.path.join(str(f["results_dir"]), "chrom_{}_{}".format(chrom, batch))
+    os.makedirs(path, exist_ok=True)
+    with open(os.path.join(path, f"flags{seed}.txt"), "w") as fh:
+        fh.write(s)
+
+    mu = np.array([float(x) for x in f["mu"]], dtype=np.float32)
+    sigma = np.array([float(x) for x in f["sigma"]], dtype=np.float32)
+    K = mu.shape[0]
+    theta = read_theta(str(f["single_group_dir"]), chrom)
+    if theta.shape[0] != K * K:
+        raise ValueError(f"theta_{chrom}.csv.gz holds {theta.shape[0]} values, expected K^2 = {K * K}")
+
+    dd = str(f["data_dir"])
+    positions = _read_matrix(os.path.join(dd, f"positions_{chrom}.txt.gz"))
+    tot_c = _read_matrix(os.path.join(dd, f"n_total_reads_control_{chrom}.txt.gz"))
+    meth_c = _read_matrix(os.path.join(dd, f"n_methylated_reads_control_{chrom}.txt.gz"))
+    tot_k = _read_matrix(os.path.join(dd, f"n_total_reads_case_{chrom}.txt.gz"))
+    meth_k = _read_matrix(os.path.join(dd, f"n_methylated_reads_case_{chrom}.txt.gz"))
+
+    seg = segment_index(positions.shape[0], batch, int(f["segment_size"]), int(f["buffer_size"]))
+    if seg is None:
+        print("Batch index is too large for the chromosome")
+        return 0
+    (lo, hi), (r0, r1) = seg
+    ob_c, ob_k = meth_c[lo:hi].astype(np.float32), meth_k[lo:hi].astype(np.float32)
+    nt_c, nt_k = tot_c[lo:hi].astype(np.float32), tot_k[lo:hi].astype(np.float32)
+    pos = positions[lo:hi].astype(np.int64)
+    if np.sum(nt_k < ob_k) != 0 or np.sum(nt_c < ob_c) != 0:
+        raise AssertionError("methylated reads exceed total reads")
+    ret = slice(r0, r1)
+
+    _savetxt(os.path.join(path, "observations_control.csv.gz"), ob_c.astype(np.int16)[ret])
+    _savetxt(os.path.join(path, "observations_case.csv.gz"), ob_k.astype(np.int16)[ret])
+    _savetxt(os.path.join(path, "n_total_reads_control.csv.gz"), nt_c.astype(np.int16)[ret])
+    _savetxt(os.path.join(path, "n_total_reads_case.csv.gz"), nt_k.astype(np.int16)[ret])
+    _savetxt(os.path.join(path, "positions.csv.gz"), pos[ret])
+
+    from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
+
+    T = hi - lo
+    max_reads = int(max(nt_c.max(initial=0), nt_k.max(initial=0)))
+    log_z: Dict[int, float] = {}
+    times: Dict[int, float] = {}
+    for M in f["num_resampled_particles"]:
+        print(M)
+        N = int(M) * (2 * K + K * K)
+        model = two_group.CaseControlModel(
+            mu, sigma, theta, minimum_duration=int(f["minimum_duration"]), omega_case=float(f["omega_case"]),
+            merge_log_prob=float(f["merge_log_prob"]), split_prob=float(f["split_prob"]),
+            num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
+            max_total_reads=max_reads, max_duration=T + 1, multinomial=bool(f["multinomial"]))
+        t0 = time.time()
+        res, _final_w, ex = two_group.run({"control": ob_c, "case": ob_k}, {"control": nt_c, "case": nt_k}, model,
+                                          seed, chain_id(chrom, batch))
+        times[N] = time.time() - t0
+        log_z[N] = float(ex["log_z"])
+        pr = res.particle
+        np.savez_compressed(os.path.join(path, f"optimal_backward_particles_merged_state_{N}_{seed}"),
+                            pr["merged_state"].astype(np.int16)[ret])
+        np.savez_compressed(os.path.join(path, f"optimal_backward_particles_control_state_{N}_{seed}"),
+                            pr["control_state"].astype(np.int16)[ret])
+        np.savez_compressed(os.path.join(path, f"optimal_backward_particles_case_state_{N}_{seed}"),
+                            pr["case_state"].astype(np.int16)[ret])
+        np.savez_compressed(os.path.join(path, f"optimal_split_probs_{N}_{seed}"), ex["split_probs"])
+        np.savez_compressed(os.path.join(path, f"optimal_regime_probs_{N}_{seed}"), ex["regime_probs"])
+        model.close()
+    with open(os.path.join(path, f"log_normalizing_constants_optimal_{seed}.txt"), "w") as fh:
+        print(log_z, file=fh)
+    with open(os.path.join(path, f"optimal_time_{seed}.txt"), "w") as fh:
+        print(times, file=fh)
+    with open(os.path.join(path, f"optimal_time_backward_{seed}.txt"), "w") as fh:
+        print({}, file=fh)
+    return 0
+
+
+COMMANDS = "preprocess get_chrom_segments infer aggregate get_dmps"
+
+
+def main(argv: Sequence[str] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv:
+        print("Usage: hygeia [command] [arguments...]")
+        return 1
+    cmd, rest = argv[0], argv[1:]
+    if cmd == "infer":
+        try:
+            return infer(rest)
+        except FlagError as e:
+            print(f"FATAL Flags parsing error: {e}", file=sys.stderr)
+            return 1
+    if cmd in ("version", "-v", "--version"):
+        from . import _lib
+        print("Hygeia version {} ({})".format(os.environ.get("HYGEIA_VERSION", ""),
+                                              _lib.load().hyg_version().decode()))
+        return 0
+    if cmd in ("help", "-h", "--help"):
+        print("Usage: hygeia [command] [arguments...]\n  infer  - Run inference on two groups (MI355X)")
+        return 0
+    if cmd in COMMANDS.split():
+        print(f"Error: '{cmd}' is not part of the MI355X inference path; use the reference pipeline step",
+              file=sys.stderr)
+        return 2
+    print(f"Error: Invalid command '{cmd}'\nValid commands are: {COMMANDS}\nUse 'hygeia help' for more information")
+    return 2
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -57,10 +57,10 @@ class CaseControlModel:
                  minimum_duration: int = 3, omega_case: float = 0.8, merge_log_prob: float = math.log(0.1),
                  split_prob: float = 0.01, num_resampled_ancestors: int = 50, num_samples_backward: int = 25,
                  kappa_control: float = 2.0, kappa_case: float = 2.0, max_total_reads: int = 1023,
-                 max_duration: int = 110000):
+                 max_duration: int = 110000, optimal_resampling: bool = True, multinomial: bool = False):
         self.params = _lib.make_params(mu, sigma, theta, minimum_duration, num_resampled_ancestors,
                                        num_samples_backward, omega_case, merge_log_prob, split_prob,
-                                       kappa_control, kappa_case)
+                                       kappa_control, kappa_case, optimal_resampling, multinomial)
         self.n_regimes = len(mu)
         self.num_resampled_ancestors = int(num_resampled_ancestors)
         self.num_samples_backward = int(num_samples_backward)

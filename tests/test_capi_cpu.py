@@ -83,8 +83,9 @@ def test_sigma_outside_beta_range_is_rejected(lib):
     assert lib.hyg_tg_model_create(C.byref(p), 200, 1000, C.byref(m)) == _lib.HYG_EINVAL
 
 
-@pytest.mark.skipif(_lib.load().hyg_device_count() > 0, reason="host without a GPU only")
 def test_compute_refuses_without_device(lib):
+    if lib.hyg_device_count() > 0:
+        pytest.skip("host without a GPU only")
     m = C.c_void_p()
     assert lib.hyg_tg_model_create(C.byref(_params()), 200, 1000, C.byref(m)) == _lib.HYG_OK
     try:

@@ -1,0 +1,118 @@
+"""`hygeia infer` host logic (hygeia_amd/cli.py) against run_inference_two_groups.py:
+flags (:19-72), segment slicing and early exit (:194-218), file layout (:101-108,
+246-322). CPU only: the compute call itself must refuse without a GPU.
+"""
+import gzip
+import math
+import os
+
+import numpy as np
+import pytest
+
+from hygeia_amd import cli
+
+
+def test_flag_defaults_match_reference():
+    f = cli.parse_flags([])
+    assert f["mu"] == ["0.95", "0.05", "0.80", "0.20", "0.50", "0.50"]
+    assert f["sigma"] == ["0.05", "0.05", "0.1", "0.1", "0.1", "0.2886751"]
+    assert f["minimum_duration"] == 3 and f["omega_case"] == 0.8
+    assert f["merge_log_prob"] == pytest.approx(math.log(0.1)) and f["split_prob"] == 0.01
+    assert f["num_resampled_particles"] == [50] and f["num_samples_backward"] == 25
+    assert f["multinomial"] is False and f["chrom"] == "22"
+    assert (f["seed"], f["batch"], f["segment_size"], f["buffer_size"]) == (0, 0, 100000, 5000)
+
+
+def test_flag_forms():
+    f = cli.parse_flags(["--mu", "0.9,0.1", "--sigma=0.05,0.05", "--chrom", "chr7", "--seed=3", "--batch", "2",
+                         "--num_resampled_particles=20", "--num_resampled_particles", "30", "--multinomial",
+                         "--segment_size", "1000", "--results_dir", "/tmp/x"])
+    assert f["mu"] == ["0.9", "0.1"] and f["sigma"] == ["0.05", "0.05"]
+    assert f["chrom"] == "chr7" and f["seed"] == 3 and f["batch"] == 2
+    assert f["num_resampled_particles"] == [20, 30] and f["multinomial"] is True
+    assert cli.parse_flags(["--nomultinomial"])["multinomial"] is False
+    with pytest.raises(cli.FlagError):
+        cli.parse_flags(["--not_a_flag=1"])
+    with pytest.raises(cli.FlagError):
+        cli.parse_flags(["--seed"])
+
+
+def test_serialized_flags_roundtrip():
+    f = cli.parse_flags(["--num_resampled_particles=20", "--num_resampled_particles=30", "--chrom=5"])
+    s = cli.serialize_flags(f)
+    assert "--num_resampled_particles=20\n--num_resampled_particles=30" in s
+    assert "--nomultinomial" in s and "--chrom=5" in s
+    assert cli.parse_flags(s.split("\n")) == f
+
+
+@pytest.mark.parametrize("n,batch,S,B,want", [
+    (250000, 0, 100000, 5000, ((0, 105000), (0, 100000))),
+    (250000, 1, 100000, 5000, ((95000, 205000), (5000, 105000))),
+    (250000, 2, 100000, 5000, ((195000, 250000), (5000, 55000))),
+    (200000, 2, 100000, 5000, ((195000, 200000), (5000, 5000))),   # b*S == n: an empty return range
+    (250000, 3, 100000, 5000, None),                                # b*S > n: exit 0
+    (50, 0, 100000, 5000, ((0, 50), (0, 50))),
+])
+def test_segment_index(n, batch, S, B, want):
+    assert cli.segment_index(n, batch, S, B) == want
+
+
+def test_segments_cover_the_chromosome_once():
+    n, S, B = 123457, 10000, 500
+    covered = np.zeros(n, int)
+    b = 0
+    while True:
+        seg = cli.segment_index(n, b, S, B)
+        if seg is None:
+            break
+        (lo, hi), (r0, r1) = seg
+        covered[lo + r0:lo + r1] += 1
+        b += 1
+    assert np.all(covered == 1)
+
+
+def _write_inputs(d, chrom, T, S=2, K=6, seed=4):
+    from hygeia_amd import synthetic as syn
+    from hygeia_amd import two_group
+
+    data = syn.simulate(T, S, S, K=K, seed=seed, coverage=30.0)
+    os.makedirs(os.path.join(d, "data"), exist_ok=True)
+    os.makedirs(os.path.join(d, "sg"), exist_ok=True)
+    pos = syn.positions(T, seed)
+    np.savetxt(os.path.join(d, "data", f"positions_{chrom}.txt.gz"), pos.astype(np.float64), fmt="%s")
+    for g in ("control", "case"):
+        np.savetxt(os.path.join(d, "data", f"n_total_reads_{g}_{chrom}.txt.gz"),
+                   data[f"tot_{g}"].astype(np.float64), fmt="%s", delimiter=",")
+        np.savetxt(os.path.join(d, "data", f"n_methylated_reads_{g}_{chrom}.txt.gz"),
+                   data[f"meth_{g}"].astype(np.float64), fmt="%s", delimiter=",")
+    theta = two_group.uniform_theta(K, 0.8)
+    with gzip.open(os.path.join(d, "sg", f"theta_{chrom}.csv.gz"), "wt") as fh:
+        fh.write("data\n" + "\n".join(repr(float(x)) for x in theta) + "\n")
+    return data
+
+
+def test_infer_too_large_batch_exits_zero(tmp_path):
+    _write_inputs(str(tmp_path), "21", 300)
+    rc = cli.main(["infer", "--chrom", "21", "--batch", "5", "--segment_size", "100",
+                   "--data_dir", str(tmp_path / "data"), "--single_group_dir", str(tmp_path / "sg"),
+                   "--results_dir", str(tmp_path / "res")])
+    assert rc == 0
+    assert os.path.exists(tmp_path / "res" / "chrom_21_5" / "flags0.txt")
+
+
+def test_infer_writes_inputs_then_refuses_without_gpu(tmp_path):
+    from hygeia_amd import _lib
+
+    if _lib.load().hyg_device_count() > 0:
+        pytest.skip("host without a GPU only")
+    data = _write_inputs(str(tmp_path), "21", 300)
+    args = ["infer", "--chrom", "21", "--batch", "1", "--segment_size", "100", "--buffer_size", "10",
+            "--data_dir", str(tmp_path / "data"), "--single_group_dir", str(tmp_path / "sg"),
+            "--results_dir", str(tmp_path / "res"), "--seed", "7"]
+    with pytest.raises(_lib.HygError) as e:
+        cli.main(args)
+    assert e.value.code == _lib.HYG_EDEVICE
+    out = tmp_path / "res" / "chrom_21_1"
+    obs = np.loadtxt(out / "observations_control.csv.gz", delimiter=",")
+    np.testing.assert_array_equal(obs, data["meth_control"][100:200])  # rows [90, 210), returned [10, 110)
+    assert (out / "flags7.txt").read_text().startswith("--mu=")

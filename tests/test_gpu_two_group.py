@@ -5,6 +5,8 @@ split and regime probabilities (f32), bit-exact log normalising constant and
 final weights (f64) -- the arithmetic contract of include/hyg_arith.h makes the
 kernels and the oracle compute the same numbers.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -53,6 +55,9 @@ CASES = [
     (6, 50, 25, 1, 4, 100.0, 17, 6),      # a single site: no filter step
     (6, 50, 25, 2, 4, 100.0, 18, 7),
     (6, 50, 25, 5, 4, 100.0, 19, 8),
+    (12, 50, 25, 300, 6, 100.0, 20, 9),   # K = 12 (config C5 regimes): N_max = 8400
+    (6, 100, 30, 400, 4, 100.0, 21, 10),  # M > 64: general weight / backward paths
+    (4, 30, 70, 300, 2, 50.0, 22, 11),    # B > 64: general backward path
 ]
 
 
@@ -195,3 +200,41 @@ def test_golden_fixture(name):
     np.testing.assert_array_equal(ex["regime_probs"], g["regime_probs"])
     assert ex["log_z"] == float(g["log_z"])
     np.testing.assert_array_equal(fw, g["final_log_weights"])
+
+
+def test_cli_infer_end_to_end(tmp_path, oracle):
+    """`hygeia infer` (hygeia_amd/cli.py) on a 3-batch chromosome: the saved,
+    trimmed trajectories and the untrimmed probabilities equal the oracle's run
+    of the same segment with the same (seed, chain id)."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_cli import _write_inputs
+
+    from hygeia_amd import cli, two_group
+
+    data = _write_inputs(str(tmp_path), "7", 2300)
+    for batch in (0, 1, 2):
+        rc = cli.main(["infer", "--chrom", "7", "--batch", str(batch), "--segment_size", "1000",
+                       "--buffer_size", "50", "--num_resampled_particles", "20", "--num_samples_backward", "8",
+                       "--seed", "3", "--data_dir", str(tmp_path / "data"),
+                       "--single_group_dir", str(tmp_path / "sg"), "--results_dir", str(tmp_path / "res")])
+        assert rc == 0
+        (lo, hi), (r0, r1) = cli.segment_index(2300, batch, 1000, 50)
+        mu = np.array([0.95, 0.05, 0.80, 0.20, 0.50, 0.50], np.float32)
+        sg = np.array([0.05, 0.05, 0.1, 0.1, 0.1, 0.2886751], np.float32)
+        p = oracle.make_params(K=6, M=20, B=8, mu=mu, sigma=sg, theta=two_group.uniform_theta(6, 0.8))
+        E = oracle.emission(p, data["meth_control"][lo:hi], data["tot_control"][lo:hi], data["meth_case"][lo:hi],
+                            data["tot_case"][lo:hi])
+        ref = oracle.chain(p, E, 3, cli.chain_id("7", batch))
+        out = tmp_path / "res" / f"chrom_7_{batch}"
+        N = 20 * 48
+        ld = lambda n: np.load(out / f"{n}_{N}_3.npz")["arr_0"]  # noqa: E731
+        np.testing.assert_array_equal(ld("optimal_backward_particles_merged_state"), ref["merged"][r0:r1])
+        np.testing.assert_array_equal(ld("optimal_backward_particles_control_state"), ref["control"][r0:r1])
+        np.testing.assert_array_equal(ld("optimal_backward_particles_case_state"), ref["case"][r0:r1])
+        np.testing.assert_array_equal(ld("optimal_split_probs"), ref["split_probs"])
+        np.testing.assert_array_equal(ld("optimal_regime_probs"), ref["regime_probs"])
+        txt = (out / "log_normalizing_constants_optimal_3.txt").read_text()
+        assert txt.startswith("{960: ")
+        assert float(txt.split(":")[1].strip(" }\n")) == pytest.approx(ref["log_z"], rel=1e-15)
