@@ -9,8 +9,10 @@ with optimal finite-state resampling, backward simulation of 25 trajectories,
 for every (chromosome segment, seed) chain. Units = trimmed CpG sites x seeds.
 
 Multi-GPU (torchrun, one rank per GPU): the chains are independent; every rank
-runs the full genome with its own seeds (weak scaling, no data-path
-collective); value = sum over ranks / max-over-ranks time.
+runs the full genome with its own seeds (weak scaling, no collective in the
+filter); each step ends with the job's gather: per-site posterior counts over all
+trajectories, summed over ranks by one RCCL all-reduce (hygeia_amd/parallel.py).
+value = sum over ranks / max-over-ranks time.
 
 Also reported: the roofline of the dominant kernel (HIP events on the launch
 stream), and the CPU oracle timed on the host cores on a bounded sample.
@@ -118,7 +120,7 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
-    from hygeia_amd import _lib, synthetic, two_group
+    from hygeia_amd import _lib, parallel, synthetic, two_group
 
     L = _lib.load()
     K, M, B = args.K, args.M, args.B
@@ -145,11 +147,24 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
     E = torch.empty((args.sites, 2 * K), dtype=torch.float64, device=dev)
+    # final gather of the job (aggregate_results.py:71-206): per-site posterior
+    # counts over all seeds' trajectories, summed over ranks by one all-reduce
+    seg_of = {(ci << 32) | b: (s0, r0, rl) for (ci, b, s0, n, r0, rl) in segs}
+    src = np.concatenate([np.arange(c[4] + seg_of[c[3]][1], c[4] + seg_of[c[3]][1] + seg_of[c[3]][2]) for c in chains])
+    dst = np.concatenate([np.arange(seg_of[c[3]][0] + seg_of[c[3]][1], seg_of[c[3]][0] + seg_of[c[3]][1]
+                                    + seg_of[c[3]][2]) for c in chains])
+    rows_out = torch.from_numpy(src).to(dev)
+    rows_site = torch.from_numpy(dst).to(dev)
+    counts = torch.zeros((args.sites, 1 + 2 * K), dtype=torch.int32, device=dev)
 
     def step():
         dc.emission(data["meth_control"], data["tot_control"], data["meth_case"], data["tot_case"], E=E,
                     stream=sp)
         dc.run(E, stream=sp)
+        with torch.cuda.stream(stream):
+            counts.zero_()
+            parallel.posterior_counts(dc.split_probs, dc.regime_probs, B, rows_out, rows_site, args.sites, counts)
+            parallel.allreduce_counts(counts)
 
     L.hyg_set_kernel_timing(1)
     for _ in range(args.warmup):
@@ -174,6 +189,10 @@ def main():
     status = dc.status.cpu().numpy()
     if (status != 0).any():
         raise RuntimeError(f"{int((status != 0).sum())} chains failed: {np.unique(status)}")
+    # every site is counted once per trajectory of every seed on every rank
+    per_site = counts[:, 1:1 + K].sum(dim=1)
+    if not bool((per_site == B * len(seeds) * world).all().item()):
+        raise RuntimeError("posterior counts do not cover every site once per trajectory")
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -187,9 +206,11 @@ def main():
     achieved = bpu * units / (kavg[dom] / 1000.0) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc):  # HBM bytes per launch from the PMC pass of the same workload
         try:
-            traffic = json.load(open(pmc)).get(names[dom])
+            pj = json.load(open(pmc))
+            if pj.get("workload_sites") == args.sites and pj.get("seeds_per_gpu") == args.seeds:
+                traffic = pj.get(names[dom])
         except Exception:
             traffic = None
     line = {

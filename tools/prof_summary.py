@@ -74,6 +74,8 @@ def main():
                 traffic[k] = per
                 w.writerow([k, fn, f"{fb:.0f}", f"{2 * fb:.0f}", f"{wb:.0f}", f"{per:.0f}"])
                 print(f"{k:30s} fetch(x2)={2 * fb / max(fn, 1) / 1e9:8.3f} GB write={wb / max(wn, 1) / 1e9:8.3f} GB")
+        traffic["workload_sites"] = int(os.environ.get("HYG_PMC_SITES", "28000000"))
+        traffic["seeds_per_gpu"] = int(os.environ.get("HYG_PMC_SEEDS", "2"))
         with open(os.path.join(PROF, "pmc_traffic.json"), "w") as f:
             json.dump(traffic, f, indent=1)
 
