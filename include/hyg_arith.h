@@ -44,9 +44,18 @@
 #else
 #include <math.h>
 #define HYG_HD static inline
-#define HYG_FLOOR(x) floor(x)
-#define HYG_FMIN(a, b) fmin(a, b)
-#define HYG_FMAX(a, b) fmax(a, b)
+/* host forms that compile inline (no libm calls) with the same results on the
+ * arguments the contract uses: floor of |v| < 2^62, maxNum/minNum semantics
+ * for a NaN first argument */
+static inline double hyg__floor(double v) {
+  const double t = (double)(long long)v;
+  return (t > v) ? t - 1.0 : t;
+}
+static inline double hyg__fmin(double a, double b) { return (a < b) ? a : ((a != a) ? b : b); }
+static inline double hyg__fmax(double a, double b) { return (a > b) ? a : ((a != a) ? b : b); }
+#define HYG_FLOOR(x) hyg__floor(x)
+#define HYG_FMIN(a, b) hyg__fmin(a, b)
+#define HYG_FMAX(a, b) hyg__fmax(a, b)
 #endif
 
 /* ------------------------------------------------------------------ bits */

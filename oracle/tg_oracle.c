@@ -426,9 +426,10 @@ int oracle_tg_chain(const hyg_tg_params* p, const double* E, int T, uint64_t see
   hyg_u192* revcum = (hyg_u192*)malloc(sizeof(hyg_u192) * (Nmax + 1));
   int* parents = (int*)malloc(sizeof(int) * (M > Nmax ? M : Nmax));
   double* logits = (double*)malloc(sizeof(double) * Nmax);
+  hyg_u128* cdfa = (hyg_u128*)malloc(sizeof(hyg_u128) * Nmax);
   uint64_t* X = (uint64_t*)malloc(sizeof(uint64_t) * B);
   if (!cx.rec || !cx.par_state || !cx.par_w || !st || !W || !lw32 || !keys || !mass || !revcum || !parents ||
-      !logits || !X) {
+      !logits || !cdfa || !X) {
     rc = HYG_ENOMEM;
     goto done;
   }
@@ -452,23 +453,40 @@ int oracle_tg_chain(const hyg_tg_params* p, const double* E, int T, uint64_t see
       for (int n = 0; n < Nmax; ++n) final_w[n] = (n < N) ? W[n] : -INFINITY;
     }
   }
-  /* ---- backward simulation (filter_and_smoother_algorithm.py:368-447) */
+  /* ---- backward simulation (filter_and_smoother_algorithm.py:368-447).
+   * Trajectory b draws from the row logits[n] = log f(X_b | x_n) + W_n
+   * (:400-435); trajectories with the same next state share the row, so it and
+   * its exact mass prefix are built once per distinct state (the draws are
+   * the categorical() results of each trajectory's own row). */
   for (int t = T - 1; t >= 0; --t) {
     N = gen_particles(&cx, t, st, W);
-    for (int b = 0; b < B; ++b) {
-      const uint64_t rnd = hyg_rand64(seed, chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
-      int idx;
-      if (t == T - 1) {
-        idx = categorical(W, N, rnd);
-      } else {
+    for (int b = 0; b < B; ++b) parents[b] = -2;
+    for (int b0 = 0; b0 < B; ++b0) {
+      if (parents[b0] != -2) continue;
+      const double* row = W;
+      if (t != T - 1) {
         for (int n = 0; n < N; ++n) {
-          const double f = hyg_isfinite(W[n]) ? tg_trans(&om, st[n], X[b]) : -INFINITY;
+          const double f = hyg_isfinite(W[n]) ? tg_trans(&om, st[n], X[b0]) : -INFINITY;
           logits[n] = (hyg_isfinite(f) && hyg_isfinite(W[n])) ? f + W[n] : -INFINITY;
         }
-        idx = categorical(logits, N, rnd);
+        row = logits;
       }
-      if (idx < 0) { rc = HYG_ENUMERIC; goto done; }
-      parents[b] = idx;
+      double lmax = -INFINITY;
+      for (int n = 0; n < N; ++n) if (row[n] > lmax) lmax = row[n];
+      if (lmax == -INFINITY) { rc = HYG_ENUMERIC; goto done; }
+      hyg_u128 run = hyg_u128_zero();
+      for (int n = 0; n < N; ++n) { run = hyg_u128_add(run, hyg_fix100(hyg_exp(row[n] - lmax))); cdfa[n] = run; }
+      for (int b = b0; b < B; ++b) {
+        if (parents[b] != -2 || (t != T - 1 && X[b] != X[b0])) continue;
+        const uint64_t rnd = hyg_rand64(seed, chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
+        const hyg_u128 target = hyg_scale_target(rnd, run);
+        int lo = 0, hi = N - 1; /* first n with target < cdf[n] (categorical()) */
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (hyg_u128_lt(target, cdfa[mid])) hi = mid; else lo = mid + 1;
+        }
+        parents[b] = lo;
+      }
     }
     int n_split = 0, nc[HYG_KMAX], nk[HYG_KMAX];
     for (int r = 0; r < K; ++r) nc[r] = nk[r] = 0;
@@ -494,7 +512,7 @@ int oracle_tg_chain(const hyg_tg_params* p, const double* E, int T, uint64_t see
   rc = HYG_OK;
 done:
   free(cx.rec); free(cx.par_state); free(cx.par_w); free(st); free(W); free(lw32); free(keys); free(mass);
-  free(revcum); free(parents); free(logits); free(X);
+  free(revcum); free(parents); free(logits); free(cdfa); free(X);
   om_free(&om);
   return rc;
 }
