@@ -70,9 +70,40 @@ class TgOutputs(C.Structure):
     ]
 
 
+class SgParams(C.Structure):
+    """Mirror of hyg_sg_params (include/hygeia_amd.h)."""
+
+    _fields_ = [
+        ("n_regimes", C.c_int32),
+        ("minimum_duration", C.c_int32),
+        ("num_particles_max", C.c_int32),
+        ("resample_type", C.c_int32),
+        ("is_kappa_fixed", C.c_int32),
+        ("theta_len", C.c_int32),
+        ("alpha", C.c_double * KMAX),
+        ("beta", C.c_double * KMAX),
+        ("kappa", C.c_double * KMAX),
+        ("theta", C.c_double * (KMAX * (KMAX + 1))),
+        ("epsilon", C.c_double),
+    ]
+
+
+class SgChain(C.Structure):
+    _fields_ = [
+        ("site_begin", C.c_int64),
+        ("n_sites", C.c_int32),
+        ("_pad", C.c_int32),
+        ("seed", C.c_uint64),
+        ("chain_id", C.c_uint64),
+        ("out_begin", C.c_int64),
+    ]
+
+
 EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy", "hyg_tg_num_particles",
            "hyg_tg_emission", "hyg_tg_workspace_bytes", "hyg_tg_run_chains", "hyg_tg_run_chain_host",
-           "hyg_device_count", "hyg_last_error", "hyg_version", "hyg_set_kernel_timing", "hyg_tg_last_kernel_ms")
+           "hyg_device_count", "hyg_last_error", "hyg_version", "hyg_set_kernel_timing", "hyg_tg_last_kernel_ms",
+           "hyg_sg_params_default", "hyg_sg_model_create", "hyg_sg_model_destroy", "hyg_sg_emission",
+           "hyg_sg_workspace_bytes", "hyg_sg_run_chains", "hyg_sg_run_chain_host")
 
 _lib = None
 
@@ -119,6 +150,20 @@ def load() -> C.CDLL:
     L.hyg_set_kernel_timing.argtypes = [C.c_int]
     L.hyg_tg_last_kernel_ms.restype = C.c_int
     L.hyg_tg_last_kernel_ms.argtypes = [C.POINTER(C.c_float)]
+    L.hyg_sg_params_default.restype = None
+    L.hyg_sg_params_default.argtypes = [C.POINTER(SgParams)]
+    L.hyg_sg_model_create.restype = C.c_int
+    L.hyg_sg_model_create.argtypes = [C.POINTER(SgParams), i32, i32, C.POINTER(vp)]
+    L.hyg_sg_model_destroy.restype = None
+    L.hyg_sg_model_destroy.argtypes = [vp]
+    L.hyg_sg_emission.restype = C.c_int
+    L.hyg_sg_emission.argtypes = [vp, vp, vp, i32, i64, vp, vp]
+    L.hyg_sg_workspace_bytes.restype = sz
+    L.hyg_sg_workspace_bytes.argtypes = [vp, i32, i32]
+    L.hyg_sg_run_chains.restype = C.c_int
+    L.hyg_sg_run_chains.argtypes = [vp, C.POINTER(SgChain), i32, vp, vp, sz, i32, vp, vp, vp]
+    L.hyg_sg_run_chain_host.restype = C.c_int
+    L.hyg_sg_run_chain_host.argtypes = [vp, vp, vp, i32, i32, u64, u64, vp]
     L.hyg_version.restype = C.c_char_p
     L.hyg_version.argtypes = []
     _lib = L

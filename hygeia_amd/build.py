@@ -15,9 +15,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libhygeia_amd.so")
-SOURCES = [os.path.join(HERE, "csrc", "capi.cpp"), os.path.join(HERE, "csrc", "tg_kernels.hip")]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", "tg_common.h")] + [
-    os.path.join(ROOT, "include", f) for f in ("hygeia_amd.h", "hyg_arith.h", "hyg_model.h")]
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("capi.cpp", "tg_kernels.hip", "sg_kernels.hip")]
+DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in ("tg_common.h", "sg_common.h", "hyg_dev.h")] + [
+    os.path.join(ROOT, "include", f) for f in ("hygeia_amd.h", "hyg_arith.h", "hyg_model.h", "hyg_sg_model.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
          "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt",

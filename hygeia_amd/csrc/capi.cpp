@@ -11,6 +11,8 @@
 
 #include "../../include/hyg_arith.h"
 #include "../../include/hygeia_amd.h"
+#include "../../include/hyg_sg_model.h"
+#include "sg_common.h"
 #include "tg_common.h"
 
 using namespace hyg;
@@ -61,6 +63,35 @@ struct hyg_tg_model {
     ModelDev m{};
     m.consts = d_consts;
     m.hz = d_hz;
+    m.dcap = dcap;
+    m.nmax_reads = nmax_reads;
+    m.lf = d_lf;
+    m.lg = d_lg;
+    m.cst = d_cst;
+    return m;
+  }
+};
+
+struct hyg_sg_model {
+  hyg_sg_consts c{};
+  int32_t dcap = 0;
+  int32_t nmax_reads = 0;
+  int32_t max_duration = 0;
+  std::vector<double> hz, lf, lg, cst;
+  std::vector<uint8_t> ex;
+  bool on_device = false;
+  hyg_sg_consts* d_consts = nullptr;
+  double* d_hz = nullptr;
+  uint8_t* d_ex = nullptr;
+  double* d_lf = nullptr;
+  double* d_lg = nullptr;
+  double* d_cst = nullptr;
+
+  SgModelDev dev() const {
+    SgModelDev m{};
+    m.consts = d_consts;
+    m.hz = d_hz;
+    m.ex = d_ex;
     m.dcap = dcap;
     m.nmax_reads = nmax_reads;
     m.lf = d_lf;
@@ -291,6 +322,192 @@ void hyg_set_kernel_timing(int enable) { set_kernel_timing(enable != 0); }
 int hyg_tg_last_kernel_ms(float* ms3) {
   if (!ms3) return fail(HYG_EINVAL, "null argument");
   return last_kernel_ms(ms3);
+}
+
+// ============================================================ single group
+
+void hyg_sg_params_default(hyg_sg_params* p) {
+  std::memset(p, 0, sizeof(*p));
+  // regimes_config defaults (bin/simulate_data:147-157), Beta moments as
+  // get_known_parameters (model_functions.R:36-59)
+  const double mu[6] = {0.95, 0.05, 0.80, 0.20, 0.50, 0.50};
+  const double sg[6] = {0.05, 0.05, 0.1, 0.1, 0.1, 0.2886751};
+  const double om[6] = {0.995, 0.975, 0.95, 0.925, 0.9, 0.9};
+  p->n_regimes = 6;
+  p->minimum_duration = 3;
+  p->num_particles_max = 250;
+  p->resample_type = 2;
+  p->is_kappa_fixed = 1;
+  p->theta_len = 36;
+  for (int i = 0; i < 6; ++i) {
+    const double nu = mu[i] * (1.0 - mu[i]) / (sg[i] * sg[i]) - 1.0;
+    p->alpha[i] = mu[i] * nu;
+    p->beta[i] = (1.0 - mu[i]) * nu;
+    p->kappa[i] = 2.0;
+  }
+  // uniform off-diagonal transitions (equal log-weights), logit(omega)
+  for (int i = 0; i < 30; ++i) p->theta[i] = std::log(1.0 / 5.0);
+  for (int i = 0; i < 6; ++i) p->theta[30 + i] = std::log(om[i] / (1.0 - om[i]));
+  p->epsilon = 0.01;
+}
+
+void hyg_sg_model_destroy(hyg_sg_model* m) {
+  if (!m) return;
+  if (m->on_device) {
+    (void)hipFree(m->d_consts);
+    (void)hipFree(m->d_hz);
+    (void)hipFree(m->d_ex);
+    (void)hipFree(m->d_lf);
+    (void)hipFree(m->d_lg);
+    (void)hipFree(m->d_cst);
+  }
+  delete m;
+}
+
+int hyg_sg_model_create(const hyg_sg_params* params, int32_t max_total_reads, int32_t max_duration,
+                        hyg_sg_model** out) {
+  if (!params || !out) return fail(HYG_EINVAL, "null argument");
+  *out = nullptr;
+  if (max_total_reads < 0 || max_total_reads > 65535) return fail(HYG_EINVAL, "max_total_reads out of [0, 65535]");
+  if (max_duration < 1 || max_duration >= HYG_DMAX - 2) return fail(HYG_EINVAL, "max_duration out of range");
+  auto* m = new hyg_sg_model();
+  int rc = hyg_sg_derive(params, &m->c);
+  if (rc != HYG_OK) {
+    delete m;
+    return fail(rc, rc == HYG_EUNSUPPORTED ? "only resample_type 2 (optimal finite state) is implemented"
+                                           : "invalid model parameters");
+  }
+  if (m->c.Nmax > kSgThreads) {
+    delete m;
+    return fail(HYG_EUNSUPPORTED, "num_particles_max > 256 (one particle per thread of a workgroup)");
+  }
+  m->max_duration = max_duration;
+  m->nmax_reads = max_total_reads;
+  m->dcap = hyg_sg_hazard_len(&m->c, max_duration + 1);
+  const int K = m->c.K, L = max_total_reads + 1;
+  m->hz.resize((size_t)K * m->dcap * 2);
+  m->ex.resize((size_t)K * m->dcap);
+  hyg_sg_hazard_fill(&m->c, m->dcap, m->hz.data(), m->ex.data());
+  m->lf.resize(L);
+  m->lg.resize((size_t)3 * K * L);
+  m->cst.resize(K);
+  hyg_sg_bb_tables(&m->c, max_total_reads, m->lf.data(), m->lg.data(), m->cst.data());
+  if (have_device()) {
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_consts, &m->c, 1);
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_hz, m->hz.data(), m->hz.size());
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_ex, m->ex.data(), m->ex.size());
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_lf, m->lf.data(), m->lf.size());
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_lg, m->lg.data(), m->lg.size());
+    if (e == hipSuccess) e = dmalloc_copy(&m->d_cst, m->cst.data(), m->cst.size());
+    m->on_device = true;
+    if (e != hipSuccess) {
+      hyg_sg_model_destroy(m);
+      return fail(HYG_EDEVICE, std::string("device upload failed: ") + hipGetErrorString(e));
+    }
+  }
+  *out = m;
+  return HYG_OK;
+}
+
+int hyg_sg_emission(const hyg_sg_model* m, const uint16_t* meth, const uint16_t* tot, int32_t n_samples,
+                    int64_t n_sites, double* E, void* stream) {
+  if (!m) return fail(HYG_EINVAL, "null model");
+  if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (n_samples < 0 || n_sites < 0) return fail(HYG_EINVAL, "negative size");
+  if (n_sites > 0 && (!E || (n_samples && (!meth || !tot)))) return fail(HYG_EINVAL, "null buffer");
+  int rc = sg_launch_emission(m->dev(), m->c, meth, tot, n_samples, n_sites, E, stream);
+  if (rc != HYG_OK) return fail(rc, "emission launch failed");
+  return HYG_OK;
+}
+
+static size_t sg_header_bytes(int32_t n_chains) {
+  const size_t h = (sizeof(SgChainDev) + sizeof(int32_t)) * (size_t)n_chains;
+  return (h + 255) / 256 * 256;
+}
+
+size_t hyg_sg_workspace_bytes(const hyg_sg_model* m, int32_t n_chains, int32_t psi_capacity) {
+  if (!m || n_chains < 0 || psi_capacity < 0) return 0;
+  const int cap = psi_capacity ? psi_capacity : kSgPsiCapDefault;
+  return sg_header_bytes(n_chains) + (size_t)n_chains * sg_chain_ws_bytes(m->c.K, cap);
+}
+
+int hyg_sg_run_chains(const hyg_sg_model* m, const hyg_sg_chain* chains, int32_t n_chains, const double* E,
+                      void* workspace, size_t workspace_bytes, int32_t psi_capacity, double* regime_probs,
+                      int32_t* status, void* stream) {
+  if (!m || !chains || !E || !workspace || !regime_probs) return fail(HYG_EINVAL, "null argument");
+  if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (n_chains <= 0) return HYG_OK;
+  if (psi_capacity < 0 || psi_capacity > (1 << 24)) return fail(HYG_EINVAL, "psi_capacity out of range");
+  const int cap = psi_capacity ? psi_capacity : kSgPsiCapDefault;
+  if (workspace_bytes < hyg_sg_workspace_bytes(m, n_chains, psi_capacity))
+    return fail(HYG_EINVAL, "workspace too small (see hyg_sg_workspace_bytes)");
+  std::vector<SgChainDev> cd(n_chains);
+  size_t off = sg_header_bytes(n_chains);
+  const size_t per = sg_chain_ws_bytes(m->c.K, cap);
+  for (int i = 0; i < n_chains; ++i) {
+    const hyg_sg_chain& c = chains[i];
+    if (c.n_sites < 1) return fail(HYG_EINVAL, "chain with no sites");
+    if (c.n_sites > m->max_duration) return fail(HYG_EINVAL, "chain longer than the model's max_duration");
+    if (c.site_begin < 0 || c.out_begin < 0) return fail(HYG_EINVAL, "negative chain offset");
+    cd[i].site_begin = c.site_begin;
+    cd[i].out_begin = c.out_begin;
+    cd[i].psi_offset = (int64_t)off;
+    cd[i].seed = c.seed;
+    cd[i].chain_id = c.chain_id;
+    cd[i].T = c.n_sites;
+    cd[i].pad = 0;
+    off += per;
+  }
+  uint8_t* ws = (uint8_t*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(ws, cd.data(), sizeof(SgChainDev) * n_chains, hipMemcpyHostToDevice, s) != hipSuccess)
+    return fail(HYG_EDEVICE, "descriptor upload failed");
+  int32_t* st = status ? status : (int32_t*)(ws + sizeof(SgChainDev) * n_chains);
+  int rc = sg_launch_chains(m->dev(), m->c, (const SgChainDev*)ws, n_chains, E, ws, cap, regime_probs, st, stream);
+  if (rc == HYG_EUNSUPPORTED) return fail(rc, "particle arrays exceed the LDS of a CU (K too large)");
+  if (rc != HYG_OK) return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  return HYG_OK;
+}
+
+int hyg_sg_run_chain_host(const hyg_sg_model* m, const uint16_t* meth, const uint16_t* tot, int32_t S, int32_t T,
+                          uint64_t seed, uint64_t chain_id, double* regime_probs) {
+  if (!m || !regime_probs || (S > 0 && (!meth || !tot))) return fail(HYG_EINVAL, "null argument");
+  if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (T < 1 || S < 0) return fail(HYG_EINVAL, "no sites");
+  for (int64_t i = 0; i < (int64_t)T * S; ++i)
+    if (tot[i] > m->nmax_reads) return fail(HYG_EINVAL, "total read count above the model's max_total_reads");
+  const int K = m->c.K;
+  struct Buf {
+    void* p = nullptr;
+    ~Buf() { if (p) (void)hipFree(p); }
+  } b_m, b_t, b_E, b_ws, b_p, b_st;
+  auto alloc = [](Buf& b, size_t n) { return hipMalloc(&b.p, n ? n : 1) == hipSuccess; };
+  const size_t nc = (size_t)T * S;
+  const size_t wsb = hyg_sg_workspace_bytes(m, 1, 0);
+  bool ok = alloc(b_m, nc * 2) && alloc(b_t, nc * 2) && alloc(b_E, sizeof(double) * T * K) && alloc(b_ws, wsb) &&
+            alloc(b_p, sizeof(double) * T * K) && alloc(b_st, 4);
+  if (!ok) return fail(HYG_ENOMEM, "device allocation failed");
+  if (nc && hipMemcpy(b_m.p, meth, nc * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (nc && hipMemcpy(b_t.p, tot, nc * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  int rc = hyg_sg_emission(m, (uint16_t*)b_m.p, (uint16_t*)b_t.p, S, T, (double*)b_E.p, nullptr);
+  if (rc) return rc;
+  hyg_sg_chain ch{};
+  ch.site_begin = 0;
+  ch.n_sites = T;
+  ch.seed = seed;
+  ch.chain_id = chain_id;
+  ch.out_begin = 0;
+  rc = hyg_sg_run_chains(m, &ch, 1, (double*)b_E.p, b_ws.p, wsb, 0, (double*)b_p.p, (int32_t*)b_st.p, nullptr);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(HYG_EDEVICE, "kernel execution failed");
+  int32_t st = 0;
+  if (hipMemcpy(&st, b_st.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(regime_probs, b_p.p, sizeof(double) * T * K, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(HYG_EDEVICE, "copy failed");
+  if (st == HYG_ENOMEM) return fail(st, "pending smoothing times exceeded psi_capacity");
+  if (st != HYG_OK) return fail(st, "all particle weights became -inf");
+  return HYG_OK;
 }
 
 }  // extern "C"

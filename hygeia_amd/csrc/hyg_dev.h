@@ -1,0 +1,249 @@
+// hyg_dev.h -- device primitives shared by the chain kernels (gfx950):
+// lane/wave ids, LDS-only workgroup barriers, DPP wave reductions and scans,
+// block reductions and scans of exact integer sums.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/hyg_arith.h"
+
+namespace hyg {
+
+// ----------------------------------------------------------- small helpers
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// wave index as a wave-uniform (SGPR) value, so branches on it are scalar
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
+// Workgroup barrier for LDS hand-offs only. __syncthreads() is a full
+// workgroup fence: it also waits for every outstanding global load and store
+// of the wave (vmcnt(0)), which would stall each step on the ancestor-history
+// stores and on the hazard-row / emission prefetches. Nothing a chain kernel
+// writes to global memory is read back by another wave of the same launch.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// ------------------------------------------------- DPP wave primitives
+// Cross-lane traffic goes through DPP (row shifts / mirrors / broadcasts,
+// a few cycles each) and v_readlane, never ds_bpermute (an LDS round trip
+// per step). Sums are exact integer sums and maxima are exact, so the
+// reduction tree is free.
+enum : int {
+  kDppQuad1032 = 0xB1,      // quad_perm [1,0,3,2]
+  kDppQuad2301 = 0x4E,      // quad_perm [2,3,0,1]
+  kDppRowMirror = 0x140,
+  kDppRowHalfMirror = 0x141,
+  kDppRowBcast15 = 0x142,
+  kDppRowBcast31 = 0x143,
+  kDppRowShr = 0x110,       // + n, n = 1..15
+};
+template <int CTRL, int RM = 0xf, int BM = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  // bound_ctrl: a lane whose source is outside its row reads 0; lanes of
+  // rows disabled by RM keep `old` = 0 as well
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, BM, true);
+}
+template <int CTRL, int RM = 0xf, int BM = 0xf>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const uint32_t lo = dpp32<CTRL, RM, BM>((uint32_t)v), hi = dpp32<CTRL, RM, BM>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double d_of(uint64_t u) { return __builtin_bit_cast(double, u); }
+__device__ __forceinline__ uint64_t u_of(double d) { return __builtin_bit_cast(uint64_t, d); }
+
+__device__ __forceinline__ double dmax(double a, double b) { return (b > a) ? b : a; }
+
+// reduce inside each 16-lane row (every lane of the row gets the row result)
+template <typename F>
+__device__ __forceinline__ double row_reduce_d(double v, F op) {
+  v = op(v, d_of(dpp64<kDppQuad1032>(u_of(v))));
+  v = op(v, d_of(dpp64<kDppQuad2301>(u_of(v))));
+  v = op(v, d_of(dpp64<kDppRowHalfMirror>(u_of(v))));
+  v = op(v, d_of(dpp64<kDppRowMirror>(u_of(v))));
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+  auto mx = [](double a, double b) { return dmax(a, b); };
+  v = row_reduce_d(v, mx);
+  const double a = d_of(rdlane64(u_of(v), 0)), b = d_of(rdlane64(u_of(v), 16));
+  const double c = d_of(rdlane64(u_of(v), 32)), d = d_of(rdlane64(u_of(v), 48));
+  return dmax(dmax(a, b), dmax(c, d));
+}
+__device__ __forceinline__ int wave_sum(int v) {
+  uint32_t x = (uint32_t)v;
+  x += dpp32<kDppQuad1032>(x);
+  x += dpp32<kDppQuad2301>(x);
+  x += dpp32<kDppRowHalfMirror>(x);
+  x += dpp32<kDppRowMirror>(x);
+  return __builtin_amdgcn_readlane((int)x, 0) + __builtin_amdgcn_readlane((int)x, 16) +
+         __builtin_amdgcn_readlane((int)x, 32) + __builtin_amdgcn_readlane((int)x, 48);
+}
+__device__ __forceinline__ hyg_u128 wave_sum128(hyg_u128 v) {
+  hyg_u128 w;
+  w.lo = dpp64<kDppQuad1032>(v.lo); w.hi = dpp64<kDppQuad1032>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppQuad2301>(v.lo); w.hi = dpp64<kDppQuad2301>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppRowHalfMirror>(v.lo); w.hi = dpp64<kDppRowHalfMirror>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppRowMirror>(v.lo); w.hi = dpp64<kDppRowMirror>(v.hi); v = hyg_u128_add(v, w);
+  hyg_u128 s = hyg_u128_zero();
+  for (int r = 0; r < 64; r += 16) {
+    hyg_u128 x;
+    x.lo = rdlane64(v.lo, r);
+    x.hi = rdlane64(v.hi, r);
+    s = hyg_u128_add(s, x);
+  }
+  return s;
+}
+
+// inclusive wave scans (Hillis-Steele inside rows, then row broadcasts)
+template <int CTRL, int RM>
+__device__ __forceinline__ hyg_u192 dpp192(hyg_u192 v) {
+  hyg_u192 r;
+  r.w0 = dpp64<CTRL, RM>(v.w0); r.w1 = dpp64<CTRL, RM>(v.w1); r.w2 = dpp64<CTRL, RM>(v.w2);
+  return r;
+}
+__device__ __forceinline__ hyg_u192 wave_incl192(hyg_u192 v) {
+  v = hyg_u192_add(v, dpp192<kDppRowShr + 1, 0xf>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowShr + 2, 0xf>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowShr + 4, 0xf>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowShr + 8, 0xf>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowBcast15, 0xa>(v));
+  v = hyg_u192_add(v, dpp192<kDppRowBcast31, 0xc>(v));
+  return v;
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ hyg_u128 dpp128(hyg_u128 v) {
+  hyg_u128 r;
+  r.lo = dpp64<CTRL, RM>(v.lo); r.hi = dpp64<CTRL, RM>(v.hi);
+  return r;
+}
+__device__ __forceinline__ hyg_u128 wave_incl128(hyg_u128 v) {
+  v = hyg_u128_add(v, dpp128<kDppRowShr + 1, 0xf>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowShr + 2, 0xf>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowShr + 4, 0xf>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowShr + 8, 0xf>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowBcast15, 0xa>(v));
+  v = hyg_u128_add(v, dpp128<kDppRowBcast31, 0xc>(v));
+  return v;
+}
+__device__ __forceinline__ int wave_incl_int(int v) {
+  uint32_t x = (uint32_t)v;
+  x += dpp32<kDppRowShr + 1, 0xf>(x);
+  x += dpp32<kDppRowShr + 2, 0xf>(x);
+  x += dpp32<kDppRowShr + 4, 0xf>(x);
+  x += dpp32<kDppRowShr + 8, 0xf>(x);
+  x += dpp32<kDppRowBcast15, 0xa>(x);
+  x += dpp32<kDppRowBcast31, 0xc>(x);
+  return (int)x;
+}
+
+// Block-wide reductions. `red` is an LDS scratch of at least 32 B per wave;
+// every call starts with a barrier so consecutive calls may reuse it.
+template <int NT>
+__device__ __forceinline__ void block_max_cnt(double m, int c, unsigned char* red, double* m_out, int* c_out) {
+  m = wave_max(m);
+  c = wave_sum(c);
+  if (NT == 64) { *m_out = m; *c_out = c; return; }
+  lds_barrier();
+  if (lane_id() == 0) {
+    ((double*)red)[2 * wave_id()] = m;
+    ((int*)red)[4 * wave_id() + 2] = c;
+  }
+  lds_barrier();
+  double mm = ((double*)red)[0];
+  int cc = ((int*)red)[2];
+  for (int w = 1; w < NT / 64; ++w) {
+    mm = dmax(mm, ((double*)red)[2 * w]);
+    cc += ((int*)red)[4 * w + 2];
+  }
+  *m_out = mm;
+  *c_out = cc;
+}
+template <int NT>
+__device__ __forceinline__ double block_max(double v, unsigned char* red) {
+  v = wave_max(v);
+  if (NT == 64) return v;
+  lds_barrier();
+  if (lane_id() == 0) ((double*)red)[wave_id()] = v;
+  lds_barrier();
+  double m = ((double*)red)[0];
+  for (int w = 1; w < NT / 64; ++w) m = dmax(m, ((double*)red)[w]);
+  return m;
+}
+template <int NT>
+__device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red) {
+  hyg_u128* r = (hyg_u128*)red;
+  v = wave_sum128(v);
+  if (NT == 64) return v;
+  lds_barrier();
+  if (lane_id() == 0) r[wave_id()] = v;
+  lds_barrier();
+  hyg_u128 s = hyg_u128_zero();
+  for (int w = 0; w < NT / 64; ++w) s = hyg_u128_add(s, r[w]);
+  return s;
+}
+
+// Exclusive block scans. The register forms return this thread's exclusive
+// prefix and the block total; the array form writes out[tid] (exclusive) and
+// out[NT] (total) for searches.
+template <int NT>
+__device__ __forceinline__ hyg_u192 block_excl192(hyg_u192 v, unsigned char* red, hyg_u192* total) {
+  hyg_u192* r = (hyg_u192*)red;
+  const hyg_u192 inc = wave_incl192(v);
+  hyg_u192 wt;  // this wave's total
+  wt.w0 = rdlane64(inc.w0, 63); wt.w1 = rdlane64(inc.w1, 63); wt.w2 = rdlane64(inc.w2, 63);
+  lds_barrier();
+  if (lane_id() == 0) r[wave_id()] = wt;
+  lds_barrier();
+  hyg_u192 pre = hyg_u192_zero(), tot = hyg_u192_zero();
+  for (int w = 0; w < NT / 64; ++w) {
+    if (w < wave_id()) pre = hyg_u192_add(pre, r[w]);
+    tot = hyg_u192_add(tot, r[w]);
+  }
+  *total = tot;
+  return hyg_u192_add(pre, hyg_u192_sub(inc, v));
+}
+template <int NT>
+__device__ __forceinline__ int block_excl_int(int v, unsigned char* red, int* total) {
+  int* r = (int*)red;
+  const int inc = wave_incl_int(v);
+  const int wt = __builtin_amdgcn_readlane(inc, 63);
+  lds_barrier();
+  if (lane_id() == 0) r[wave_id()] = wt;
+  lds_barrier();
+  int pre = 0, tot = 0;
+  for (int w = 0; w < NT / 64; ++w) {
+    if (w < wave_id()) pre += r[w];
+    tot += r[w];
+  }
+  *total = tot;
+  return pre + inc - v;
+}
+template <int NT>
+__device__ __forceinline__ void block_scan128(hyg_u128 v, hyg_u128* out, unsigned char* red) {
+  hyg_u128* r = (hyg_u128*)red;
+  const hyg_u128 inc = wave_incl128(v);
+  hyg_u128 wt;
+  wt.lo = rdlane64(inc.lo, 63); wt.hi = rdlane64(inc.hi, 63);
+  lds_barrier();
+  if (lane_id() == 0) r[wave_id()] = wt;
+  lds_barrier();
+  hyg_u128 pre = hyg_u128_zero(), tot = hyg_u128_zero();
+  for (int w = 0; w < NT / 64; ++w) {
+    if (w < wave_id()) pre = hyg_u128_add(pre, r[w]);
+    tot = hyg_u128_add(tot, r[w]);
+  }
+  hyg_u128 e2;  // inc - v
+  e2.lo = inc.lo - v.lo;
+  e2.hi = inc.hi - v.hi - (inc.lo < v.lo ? 1u : 0u);
+  out[threadIdx.x] = hyg_u128_add(pre, e2);
+  if (threadIdx.x == 0) out[NT] = tot;
+}
+
+
+}  // namespace hyg

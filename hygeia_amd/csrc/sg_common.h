@@ -1,0 +1,54 @@
+// Internal types of the single-group path shared by capi.cpp and
+// sg_kernels.hip (not part of the public ABI).
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/hyg_sg_model.h"
+
+namespace hyg {
+
+constexpr int kSgThreads = 256;         // one particle per thread: N_max <= 256
+constexpr int kSgPsiCapDefault = 4096;  // pending smoothing times per chain
+constexpr int kSgRngSystematic = 5;     // Philox stream of the systematic uniform
+
+struct SgModelDev {
+  const hyg_sg_consts* consts;  // device copy
+  const double* hz;             // [K][dcap][2]: log rho, log(1 - rho) | -inf
+  const uint8_t* ex;            // [K][dcap] exit status
+  int32_t dcap;
+  int32_t nmax_reads;
+  const double* lf;             // BB tables as hyg_sg_bb_tables
+  const double* lg;
+  const double* cst;
+};
+
+struct SgChainDev {
+  int64_t site_begin;
+  int64_t out_begin;
+  int64_t psi_offset;  // byte offset of the chain's smoothing slots in the workspace
+  uint64_t seed;
+  uint64_t chain_id;
+  int32_t T;
+  int32_t pad;
+};
+
+// Per-chain workspace: cap psi slots [K][256] f64, then the pending-time lists
+// slot[2][cap] / time[2][cap] (double-buffered), keep[cap], free[cap] (int32).
+__host__ __device__ inline size_t sg_psi_region_bytes(int K, int cap) {
+  return ((sizeof(double) * (size_t)K * kSgThreads * (size_t)cap) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t sg_chain_ws_bytes(int K, int cap) {
+  return sg_psi_region_bytes(K, cap) + ((sizeof(int32_t) * 6 * (size_t)cap) + 255) / 256 * 256;
+}
+
+int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint16_t* meth, const uint16_t* tot,
+                       int S, int64_t n_sites, double* E, void* stream);
+int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
+                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream);
+size_t sg_lds_bytes(const hyg_sg_consts& c);
+
+}  // namespace hyg

@@ -153,6 +153,72 @@ int hyg_tg_run_chain_host(const hyg_tg_model* model, const uint16_t* meth_ctrl, 
 void hyg_set_kernel_timing(int enable);
 int hyg_tg_last_kernel_ms(float* ms3);
 
+/* ======================================================== single group
+ * The single-group engine (src/single_group/src/cpp): SMC over the semi-Markov
+ * state (d, r) with up to N_max particles, optimal finite-state resampling and
+ * online marginal smoothing of the regime indicators (Alenlov & Olsson 2019),
+ * as exported to R by
+ *   runOnlineCombinedInferenceCpp(vartheta, thetaInit, genomicPositions,
+ *       nTotalReads [S x T], nMethylatedReads [S x T], nParticlesMax,
+ *       smcProposalType = 1, smcResampleType = 2, useOnlineMarginalSmoothing,
+ *       epsilon, useOnlineParameterEstimation = false, ...)
+ *     -> regimeProbabilityEstimates [T][1 + K] (position, P(r = 1..K))
+ *   (singleGroup.cpp:76-189; called by bin/estimate_parameters_and_regimes:303-322).
+ * Online parameter estimation (useOnlineParameterEstimation) is not part of
+ * this path. */
+typedef struct hyg_sg_params {
+  int32_t n_regimes;          /* K = vartheta[1] (model_functions.R:36-59)          */
+  int32_t minimum_duration;   /* u = vartheta[0]                                    */
+  int32_t num_particles_max;  /* nParticlesMax, 250 in the pipeline                 */
+  int32_t resample_type;      /* smcResampleType: 2 = optimal finite state (only)    */
+  int32_t is_kappa_fixed;     /* vartheta[2K+2]                                     */
+  int32_t theta_len;          /* K(K-1) + K (+ K if kappa is estimated)             */
+  double alpha[HYG_KMAX];     /* vartheta[2 .. K+1]                                  */
+  double beta[HYG_KMAX];      /* vartheta[K+2 .. 2K+1]                               */
+  double kappa[HYG_KMAX];     /* vartheta[2K+3 ..] when fixed                        */
+  double theta[HYG_KMAX * (HYG_KMAX + 1)]; /* K rows of K-1 log-weights of P, K logit(omega), (K log kappa) */
+  double epsilon;             /* smoothing variance threshold, 0.01                  */
+} hyg_sg_params;
+
+typedef struct hyg_sg_model hyg_sg_model;
+
+/* One chain: the sites [site_begin, site_begin + n_sites) of the site-major
+ * count arrays (one sample group on one chromosome). */
+typedef struct hyg_sg_chain {
+  int64_t site_begin;
+  int32_t n_sites;
+  int32_t _pad;
+  uint64_t seed;
+  uint64_t chain_id;
+  int64_t out_begin;
+} hyg_sg_chain;
+
+void hyg_sg_params_default(hyg_sg_params* p);
+/* Derived quantities of ModelParameters::setKnownParameters/setUnknownParameters
+ * (singleGroup.h:173-335): P, omega, kappa and the hazard tables rho(d, r)
+ * with the exit status, Beta-Binomial lgamma tables for counts <= max_total_reads. */
+int hyg_sg_model_create(const hyg_sg_params* params, int32_t max_total_reads, int32_t max_duration,
+                        hyg_sg_model** out);
+void hyg_sg_model_destroy(hyg_sg_model* model);
+/* E[t][r] = sum_s log BetaBinomial(meth_ts | tot_ts, alpha_r, beta_r)
+ * (Model::evaluateLogObservationDensity, singleGroup.h:611-627). Device pointers, [T][S]. */
+int hyg_sg_emission(const hyg_sg_model* model, const uint16_t* meth, const uint16_t* tot, int32_t n_samples,
+                    int64_t n_sites, double* emission, void* stream);
+/* Workspace for n_chains chains with room for `psi_capacity` pending smoothing
+ * times per chain (the online-smoothing state; 0 = default 4096). */
+size_t hyg_sg_workspace_bytes(const hyg_sg_model* model, int32_t n_chains, int32_t psi_capacity);
+/* Runs SMC + online marginal smoothing for n_chains chains (one workgroup
+ * each). regime_probs [rows][K] f64 receives the smoothed P(r_t = r) of every
+ * site (OnlineCombinedInference.h:106-117), status [n_chains] HYG_OK /
+ * HYG_ENUMERIC / HYG_ENOMEM (pending smoothing times exceeded psi_capacity). */
+int hyg_sg_run_chains(const hyg_sg_model* model, const hyg_sg_chain* chains, int32_t n_chains,
+                      const double* emission, void* workspace, size_t workspace_bytes, int32_t psi_capacity,
+                      double* regime_probs, int32_t* status, void* stream);
+/* Host-pointer convenience for one chain: counts [T][S]. */
+int hyg_sg_run_chain_host(const hyg_sg_model* model, const uint16_t* meth, const uint16_t* tot,
+                          int32_t n_samples, int32_t n_sites, uint64_t seed, uint64_t chain_id,
+                          double* regime_probs);
+
 /* Number of visible HIP devices (0 when none: compute calls then fail). */
 int hyg_device_count(void);
 const char* hyg_last_error(void);

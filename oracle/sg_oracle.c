@@ -1,0 +1,402 @@
+/*
+ * sg_oracle.c -- CPU oracle of the single-group engine (TEST INFRASTRUCTURE).
+ *
+ * Plain-C restatement of src/single_group/src/cpp (C++/Armadillo, R RNG):
+ *   - SMC for the change-point model        algorithms/Smc.h:114-188 (initialise),
+ *                                           :190-286 (iterate), :406-450 (resampleCp),
+ *                                           :504-522 (sampleParticlesCp), :536-574
+ *                                           (computeWeightsCp), :576-579 (selfNormalise)
+ *   - optimal finite-state resampling        misc/resample.h:289-409, systematicBase :85-117
+ *   - backward kernels                       algorithms/Smc.h:288-326
+ *   - online marginal smoothing (epsilon)    algorithms/OnlineMarginalSmoothing.h:52-255
+ *   - driver                                 algorithms/OnlineCombinedInference.h:48-118
+ *   - model                                  singleGroup.h:556-627 (initial, transition,
+ *                                            observation densities), include/hyg_sg_model.h
+ * with the arithmetic contract of include/hyg_arith.h: every sum of weights,
+ * masses or products is an exact fixed-point sum (u128, 2^-100 units), the
+ * elementary functions are hyg_exp / hyg_log, the uniform of the systematic
+ * draw comes from Philox (stream HYG_RNG_SG_SYSTEMATIC). Against the reference
+ * (R RNG, sequential double sums, not buildable here: RcppArmadillo absent)
+ * the results are "parity unpinned"; tests/test_sg_oracle.py pins the model
+ * tables and the statistical behaviour. Only used by tests/ and bench.py.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/hyg_arith.h"
+#include "../include/hyg_sg_model.h"
+
+#define HYG_RNG_SG_SYSTEMATIC 5
+
+typedef struct {
+  hyg_sg_consts c;
+  int dcap;
+  double* hz;
+  uint8_t* ex;
+} sg_model;
+
+static int sgm_init(sg_model* m, const hyg_sg_params* p, int max_duration) {
+  int rc = hyg_sg_derive(p, &m->c);
+  if (rc) return rc;
+  m->dcap = hyg_sg_hazard_len(&m->c, max_duration);
+  m->hz = (double*)malloc(sizeof(double) * 2 * (size_t)m->c.K * m->dcap);
+  m->ex = (uint8_t*)malloc((size_t)m->c.K * m->dcap);
+  if (!m->hz || !m->ex) return HYG_ENOMEM;
+  hyg_sg_hazard_fill(&m->c, m->dcap, m->hz, m->ex);
+  return HYG_OK;
+}
+static void sgm_free(sg_model* m) { free(m->hz); free(m->ex); }
+
+/* Model::evaluateLogTransitionDensity (singleGroup.h:569-608) for the two
+ * cases the change-point SMC evaluates: (1, r') from (d, r) and (d+1, r) from (d, r). */
+static double sg_trans(const sg_model* m, int dc, int rc, int dp, int rp) {
+  const int K = m->c.K;
+  int d = dp - 1;
+  if (d >= m->dcap) d = m->dcap - 1;
+  const double* h = m->hz + ((size_t)rp * m->dcap + d) * 2;
+  const int ex = m->ex[(size_t)rp * m->dcap + d];
+  if (dc == 1 && rc != rp && dp >= m->c.u) {
+    const double lp = m->c.logP[rp * K + rc];
+    return ex ? lp : (h[0] + lp);
+  }
+  if (dc > 1 && rc == rp) return h[1];
+  return -INFINITY;
+}
+
+/* exact log-sum-exp: max + log(sum fix100(exp(x - max))) */
+static double lse(const double* x, int n) {
+  double mx = -INFINITY;
+  for (int i = 0; i < n; ++i) if (x[i] > mx) mx = x[i];
+  if (!(mx > -INFINITY)) return -INFINITY;
+  hyg_u128 s = hyg_u128_zero();
+  for (int i = 0; i < n; ++i) s = hyg_u128_add(s, hyg_fix100(hyg_exp(x[i] - mx)));
+  return mx + hyg_log(hyg_u128_to_f64(s, 100));
+}
+/* exact sum of non-negative doubles <= 1 (products of probabilities) */
+static double xsum(const double* v, int n) {
+  hyg_u128 s = hyg_u128_zero();
+  for (int i = 0; i < n; ++i) s = hyg_u128_add(s, hyg_fix100(v[i]));
+  return hyg_u128_to_f64(s, 100);
+}
+
+/* descending by value, ties by ascending index (arma::sort_index "descend") */
+static const double* g_sort_v;
+static int cmp_desc(const void* a, const void* b) {
+  const int i = *(const int*)a, j = *(const int*)b;
+  if (g_sort_v[i] > g_sort_v[j]) return -1;
+  if (g_sort_v[i] < g_sort_v[j]) return 1;
+  return (i < j) ? -1 : (i > j);
+}
+static void sort_desc(const double* v, int n, int* idx) {
+  for (int i = 0; i < n; ++i) idx[i] = i;
+  g_sort_v = v;
+  qsort(idx, (size_t)n, sizeof(int), cmp_desc);
+}
+
+/* ceil(T * R) for a double T in [0, 1] and R < 2^127 (exact, via u192) */
+static hyg_u128 ceil_mul_f64(double T, hyg_u128 R) {
+  hyg_u128 z = hyg_u128_zero();
+  if (!(T > 0.0)) return z;
+  const uint64_t b = hyg_f64_bits(T);
+  const int E = (int)((b >> 52) & 0x7ff);
+  const uint64_t m = (E == 0) ? (b & 0x000fffffffffffffull) : ((b & 0x000fffffffffffffull) | 0x0010000000000000ull);
+  const int s = (E == 0) ? 1074 : 1075 - E; /* T = m 2^-s, s >= 52 for T <= 1 */
+  /* P = m * R (m < 2^53, R < 2^127: P < 2^180) as three 64-bit words */
+  const uint64_t l0 = m * R.lo, h0 = hyg_mulhi64(m, R.lo);
+  const uint64_t l1 = m * R.hi, h1 = hyg_mulhi64(m, R.hi);
+  uint64_t w0 = l0, w1 = h0 + l1, w2 = h1 + (w1 < h0 ? 1u : 0u);
+  if (s >= 192) return (w0 | w1 | w2) ? (hyg_u128){1, 0} : z;
+  /* ceil(P / 2^s): add 2^s - 1 then shift */
+  uint64_t b0 = 0, b1 = 0, b2 = 0;
+  if (s < 64) b0 = (1ull << s) - 1;
+  else if (s < 128) { b0 = ~0ull; b1 = (s == 64) ? 0 : (1ull << (s - 64)) - 1; }
+  else { b0 = ~0ull; b1 = ~0ull; b2 = (s == 128) ? 0 : (1ull << (s - 128)) - 1; }
+  const uint64_t q0 = w0 + b0, c0 = q0 < w0;
+  const uint64_t t1 = w1 + b1, c1a = t1 < w1;
+  const uint64_t q1 = t1 + c0, c1b = q1 < t1;
+  const uint64_t q2 = w2 + b2 + c1a + c1b;
+  hyg_u128 r;
+  if (s < 64) { r.lo = (q0 >> s) | (s ? q1 << (64 - s) : 0); r.hi = (q1 >> s) | (s ? q2 << (64 - s) : 0); }
+  else if (s == 64) { r.lo = q1; r.hi = q2; }
+  else if (s < 128) { r.lo = (q1 >> (s - 64)) | (q2 << (128 - s)); r.hi = q2 >> (s - 64); }
+  else if (s == 128) { r.lo = q2; r.hi = 0; }
+  else { r.lo = q2 >> (s - 128); r.hi = 0; }
+  return r;
+}
+
+typedef struct {
+  int time;
+  double* psi; /* [K][Nmax] */
+} pending_t;
+
+/* One chain over T sites: E [T][K] emission table. Writes probs [T][K]
+ * (the smoothed regime probabilities). Returns HYG_OK / HYG_ENUMERIC / HYG_ENOMEM. */
+int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t seed, uint64_t chain_id,
+                    double* probs, int32_t* nparts_out) {
+  if (T < 1 || T >= HYG_DMAX - 2) return HYG_EINVAL;
+  sg_model mo;
+  int rc = sgm_init(&mo, p, T + 1);
+  if (rc) return rc;
+  const hyg_sg_consts* c = &mo.c;
+  const int K = c->K, Nmax = c->Nmax;
+  int *dP = malloc(sizeof(int) * Nmax), *rP = malloc(sizeof(int) * Nmax), *dC = malloc(sizeof(int) * Nmax),
+      *rC = malloc(sizeof(int) * Nmax), *anc = malloc(sizeof(int) * Nmax), *idx = malloc(sizeof(int) * Nmax);
+  double *lwP = malloc(sizeof(double) * Nmax), *lwC = malloc(sizeof(double) * Nmax),
+         *wP = malloc(sizeof(double) * Nmax), *wC = malloc(sizeof(double) * Nmax),
+         *lwres = malloc(sizeof(double) * Nmax), *tmp = malloc(sizeof(double) * Nmax),
+         *tmp2 = malloc(sizeof(double) * Nmax), *logq = malloc(sizeof(double) * Nmax),
+         *BK = malloc(sizeof(double) * HYG_KMAX * Nmax);
+  hyg_u128* cum = malloc(sizeof(hyg_u128) * (Nmax + 1));
+  int cap = 64, npend = 0;
+  pending_t* pend = malloc(sizeof(pending_t) * cap);
+  if (!dP || !rP || !dC || !rC || !anc || !idx || !lwP || !lwC || !wP || !wC || !lwres || !tmp || !tmp2 || !logq ||
+      !BK || !cum || !pend) {
+    rc = HYG_ENOMEM;
+    goto done;
+  }
+  for (int t = 0; t < T; ++t)
+    for (int r = 0; r < K; ++r) probs[(size_t)t * K + r] = NAN;
+
+  /* ---- t = 0 (Smc.h:114-188): N = K particles (1, r), w = -log K + log g_0 */
+  int N = K;
+  for (int n = 0; n < N; ++n) {
+    dC[n] = 1;
+    rC[n] = n;
+    lwC[n] = -c->log_K + E[n];
+  }
+  double logZ = lse(lwC, N);
+  if (!(logZ > -INFINITY)) { rc = HYG_ENUMERIC; goto done; }
+  for (int n = 0; n < N; ++n) wC[n] = hyg_exp(lwC[n] - logZ);
+  if (nparts_out) nparts_out[0] = N;
+
+  /* psi bookkeeping (OnlineMarginalSmoothing.h:132-150 initialisePsi, :199-253 storeEstimates) */
+#define ADD_PENDING(tt)                                                              \
+  do {                                                                               \
+    if (npend == cap) {                                                              \
+      cap *= 2;                                                                      \
+      pending_t* np_ = realloc(pend, sizeof(pending_t) * cap);                       \
+      if (!np_) { rc = HYG_ENOMEM; goto done; }                                      \
+      pend = np_;                                                                    \
+    }                                                                                \
+    pend[npend].time = (tt);                                                         \
+    pend[npend].psi = malloc(sizeof(double) * K * Nmax);                             \
+    if (!pend[npend].psi) { rc = HYG_ENOMEM; goto done; }                            \
+    for (int r_ = 0; r_ < K; ++r_)                                                   \
+      for (int n_ = 0; n_ < N; ++n_) pend[npend].psi[r_ * Nmax + n_] = (rC[n_] == r_) ? 1.0 : 0.0; \
+    ++npend;                                                                         \
+  } while (0)
+
+  ADD_PENDING(0);
+  for (int t = 0; t < T; ++t) {
+    const int final = (t == T - 1);
+    if (t > 0) {
+      /* ---- Smc::iterate (:190-286) */
+      const int Np = N;
+      memcpy(dP, dC, sizeof(int) * Np);
+      memcpy(rP, rC, sizeof(int) * Np);
+      memcpy(lwP, lwC, sizeof(double) * Np);
+      memcpy(wP, wC, sizeof(double) * Np);
+      const double logZp = logZ;
+      N = (Np + K > Nmax) ? Nmax : Np + K;
+      const int M = N - K;
+      /* resampleCp (:406-450) */
+      if (N < Np + K) {
+        int fin = 0;
+        for (int n = 0; n < Np; ++n) fin += hyg_isfinite(lwP[n]) ? 1 : 0;
+        int keep_top = 1;
+        if (fin > M) {
+          /* optimalFiniteState (resample.h:289-409) on the self-normalised weights */
+          sort_desc(wP, Np, idx);
+          for (int q = 0; q < Np; ++q) logq[q] = hyg_log(wP[idx[q]]);
+          cum[Np] = hyg_u128_zero(); /* reverse cumulative sums Q(k), exact */
+          for (int q = Np - 1; q >= 0; --q) cum[q] = hyg_u128_add(cum[q + 1], hyg_fix100(wP[idx[q]]));
+          int kOld = 1, kNew = 0;
+          double logC = 0.0;
+          while (kNew != kOld) {
+            kOld = kNew;
+            const double Qk = hyg_u128_to_f64(cum[kOld], 100);
+            logC = hyg_log((double)(M - kOld)) - hyg_log(Qk);
+            int cnt = 0;
+            for (int q = kOld; q < Np; ++q) cnt += (logq[q] > -logC) ? 1 : 0;
+            kNew = kOld + cnt;
+          }
+          if (hyg_isfinite(logC)) {
+            keep_top = 0;
+            const int Kk = kNew, L = M - Kk;
+            for (int q = 0; q < Kk; ++q) {
+              anc[q] = idx[q];
+              lwres[q] = lwP[idx[q]];
+            }
+            if (L > 0) {
+              /* residual systematic draw: normalised exp(logQ[K..N)) (:372-377),
+               * systematicBase (:85-117) with T_j = (j + u) / L <= Q_i as exact
+               * C_i >= ceil(T_j * R) */
+              double rmax = -INFINITY;
+              for (int q = Kk; q < Np; ++q) if (logq[q] > rmax) rmax = logq[q];
+              hyg_u128 run = hyg_u128_zero();
+              for (int q = Kk; q < Np; ++q) {
+                run = hyg_u128_add(run, hyg_fix100(hyg_exp(logq[q] - rmax)));
+                cum[q] = run;
+              }
+              const double uu =
+                  (double)(hyg_rand64(seed, chain_id, HYG_RNG_SG_SYSTEMATIC, (uint64_t)t, 0) >> 11) *
+                  1.1102230246251565404e-16;
+              int i = Kk;
+              for (int j = 0; j < L; ++j) {
+                const double Tj = ((double)j + uu) / (double)L;
+                const hyg_u128 thr = ceil_mul_f64(Tj, run);
+                while (i < Np - 1 && hyg_u128_lt(cum[i], thr)) ++i;
+                anc[Kk + j] = idx[i];
+                lwres[Kk + j] = logZp - logC;
+              }
+            }
+          }
+        }
+        if (keep_top) {
+          /* keep the M largest weights (:432-441 and resample.h:379-384) */
+          sort_desc(lwP, Np, idx);
+          for (int n = 0; n < M; ++n) {
+            anc[n] = idx[n];
+            lwres[n] = lwP[idx[n]];
+          }
+        }
+      } else {
+        for (int n = 0; n < M; ++n) {
+          anc[n] = n;
+          lwres[n] = lwP[n];
+        }
+      }
+      /* sampleParticlesCp (:504-522) + computeWeightsCp (:536-574) */
+      const double* Et = E + (size_t)t * K;
+      for (int n = 0; n < M; ++n) {
+        dC[n] = dP[anc[n]] + 1;
+        rC[n] = rP[anc[n]];
+        lwC[n] = lwres[n] + (sg_trans(&mo, dC[n], rC[n], dP[anc[n]], rP[anc[n]]) + Et[rC[n]]);
+      }
+      for (int q = 0; q < K; ++q) {
+        dC[M + q] = 1;
+        rC[M + q] = q;
+        for (int n = 0; n < Np; ++n) tmp[n] = (sg_trans(&mo, 1, q, dP[n], rP[n]) + Et[q]) + lwP[n];
+        lwC[M + q] = lse(tmp, Np);
+      }
+      logZ = lse(lwC, N); /* selfNormaliseWeights (:576-579) */
+      if (!(logZ > -INFINITY)) { rc = HYG_ENUMERIC; goto done; }
+      for (int n = 0; n < N; ++n) wC[n] = hyg_exp(lwC[n] - logZ);
+      if (nparts_out) nparts_out[t] = N;
+      /* evaluateBackwardKernels (:288-326): K_q(n) = normalise(W_prev[n] + log f((1,q) | n)) */
+      for (int q = 0; q < K; ++q) {
+        for (int n = 0; n < Np; ++n) tmp[n] = lwP[n] + sg_trans(&mo, 1, q, dP[n], rP[n]);
+        const double lz = lse(tmp, Np);
+        for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = (lz > -INFINITY) ? hyg_exp(tmp[n] - lz) : 0.0;
+      }
+      /* updatePsi (:152-197) for every pending time */
+      for (int s = 0; s < npend; ++s) {
+        double* ps = pend[s].psi;
+        for (int r = 0; r < K; ++r) {
+          double* row = ps + r * Nmax;
+          memcpy(tmp2, row, sizeof(double) * Np);
+          for (int n = 0; n < M; ++n) row[n] = tmp2[anc[n]];
+          for (int q = 0; q < K; ++q) {
+            for (int n = 0; n < Np; ++n) tmp[n] = BK[q * Nmax + n] * tmp2[n];
+            row[M + q] = xsum(tmp, Np);
+          }
+        }
+      }
+      ADD_PENDING(t);
+    }
+    /* storeEstimates (:199-253): finalise a time once every regime's filtered
+     * variance is below epsilon (or at the final step) */
+    int keep = 0;
+    for (int s = 0; s < npend; ++s) {
+      double* ps = pend[s].psi;
+      double mean[HYG_KMAX];
+      int ok = 1;
+      for (int r = 0; r < K; ++r) {
+        const double* row = ps + r * Nmax;
+        for (int n = 0; n < N; ++n) tmp[n] = wC[n] * row[n];
+        mean[r] = xsum(tmp, N);
+        if (!final && ok) {
+          for (int n = 0; n < N; ++n) {
+            const double v = row[n] - mean[r];
+            tmp[n] = wC[n] * (v * v);
+          }
+          if (!(xsum(tmp, N) < c->epsilon)) ok = 0;
+        }
+      }
+      if (final || ok) {
+        for (int r = 0; r < K; ++r) probs[(size_t)pend[s].time * K + r] = mean[r];
+        free(ps);
+      } else {
+        pend[keep++] = pend[s];
+      }
+    }
+    npend = keep;
+  }
+  rc = HYG_OK;
+done:
+  for (int s = 0; s < npend; ++s) free(pend[s].psi);
+  free(pend);
+  free(dP); free(rP); free(dC); free(rC); free(anc); free(idx);
+  free(lwP); free(lwC); free(wP); free(wC); free(lwres); free(tmp); free(tmp2); free(logq); free(BK); free(cum);
+  sgm_free(&mo);
+  return rc;
+#undef ADD_PENDING
+}
+
+/* E[t][r] = sum_s BB(y | n, alpha_r, beta_r) (singleGroup.h:611-627, misc.h:630-640),
+ * every sample included (n = 0 adds the lgamma round-off, as the reference) */
+int oracle_sg_emission(const hyg_sg_params* p, const uint16_t* meth, const uint16_t* tot, int S, int64_t T,
+                       double* E) {
+  hyg_sg_consts c;
+  int rc = hyg_sg_derive(p, &c);
+  if (rc) return rc;
+  int nmax = 0;
+  for (int64_t i = 0; i < T * S; ++i) if (tot[i] > nmax) nmax = tot[i];
+  const int L = nmax + 1, K = c.K;
+  double* lf = malloc(sizeof(double) * L);
+  double* lg = malloc(sizeof(double) * 3 * K * L);
+  double cst[HYG_KMAX];
+  if (!lf || !lg) { free(lf); free(lg); return HYG_ENOMEM; }
+  hyg_sg_bb_tables(&c, nmax, lf, lg, cst);
+  for (int64_t t = 0; t < T; ++t) {
+    for (int r = 0; r < K; ++r) {
+      double e = 0.0;
+      for (int s = 0; s < S; ++s) {
+        const int n = tot[t * S + s], y = meth[t * S + s];
+        if (y > n) { e = -INFINITY; break; }
+        double term = (lf[n] - lf[y]) - lf[n - y];
+        term = term + lg[(size_t)(r * 3 + 0) * L + y];
+        term = term + lg[(size_t)(r * 3 + 1) * L + (n - y)];
+        term = term - lg[(size_t)(r * 3 + 2) * L + n];
+        term = term + cst[r];
+        e = e + term;
+      }
+      E[t * K + r] = e;
+    }
+  }
+  free(lf);
+  free(lg);
+  return HYG_OK;
+}
+
+/* tables for tests */
+int oracle_sg_hazard(const hyg_sg_params* p, int r, int n, double* out, uint8_t* ex, int32_t* dcap) {
+  sg_model mo;
+  int rc = sgm_init(&mo, p, n + 2);
+  if (rc) return rc;
+  *dcap = mo.dcap;
+  for (int dp = 1; dp <= n; ++dp) {
+    int d = dp - 1;
+    if (d >= mo.dcap) d = mo.dcap - 1;
+    out[2 * (dp - 1) + 0] = mo.hz[((size_t)r * mo.dcap + d) * 2 + 0];
+    out[2 * (dp - 1) + 1] = mo.hz[((size_t)r * mo.dcap + d) * 2 + 1];
+    ex[dp - 1] = mo.ex[(size_t)r * mo.dcap + d];
+  }
+  sgm_free(&mo);
+  return HYG_OK;
+}
+int oracle_sg_consts(const hyg_sg_params* p, hyg_sg_consts* out) { return hyg_sg_derive(p, out); }
+int oracle_sizeof_sg_params(void) { return (int)sizeof(hyg_sg_params); }
+int oracle_sizeof_sg_consts(void) { return (int)sizeof(hyg_sg_consts); }

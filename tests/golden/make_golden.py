@@ -12,6 +12,13 @@ Fixtures (npz, inputs + expected outputs):
   tg_chain_k6.npz    T=2000, 2+2 samples, K=6, M=10, B=5, coverage 30 (SURVEY.md 8c iv)
   tg_chain_k4.npz    T=700, 3+2 samples, K=4, M=50, B=25, coverage 100, a zero-coverage stretch
   tg_tables.npz      BB emission grid + hazard rows (log rho, log 1-rho) for the pipeline defaults
+  sg_chain_k6.npz    single group (oracle/sg_oracle.c): T=3000, S=2, K=6, pipeline defaults
+                     (N_max=250, epsilon=0.01, u=3), coverage 12
+  sg_chain_k3.npz    single group: T=800, S=3, K=3, N_max=20, epsilon=1e-4, u=2, a zero-coverage stretch
+
+The single-group oracle is pinned by tests/test_sg_oracle.py (exact semi-Markov
+smoother without resampling, scipy tables).
+``python tests/golden/make_golden.py sg`` regenerates only the sg_* fixtures.
 """
 from __future__ import annotations
 
@@ -26,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 from hygeia_amd import synthetic as syn  # noqa: E402
 from oracle import binding as ob  # noqa: E402
+from oracle import sg_binding as sb  # noqa: E402
 
 CHAINS = {
     "tg_chain_k6": dict(K=6, M=10, B=5, T=2000, S=(2, 2), coverage=30.0, data_seed=11, seed=0, chain_id=3),
@@ -65,10 +73,43 @@ def tables_fixture():
     np.savez_compressed(os.path.join(HERE, "tg_tables.npz"), meth=meth, tot=tot, E=E, hazard=hz)
 
 
+SG_CHAINS = {
+    "sg_chain_k6": dict(K=6, T=3000, S=2, coverage=12.0, data_seed=31, seed=4, chain_id=(21 << 32) | 1,
+                        u=3, Nmax=250, epsilon=0.01, omega=None),
+    "sg_chain_k3": dict(K=3, T=800, S=3, coverage=8.0, data_seed=32, seed=9, chain_id=5, u=2, Nmax=20,
+                        epsilon=1e-4, omega=(0.9, 0.85, 0.95), zero=(200, 260)),
+}
+
+
+def sg_chain_fixture(name, K, T, S, coverage, data_seed, seed, chain_id, u, Nmax, epsilon, omega, zero=None):
+    mu, sg = syn.regime_params(K)
+    d = syn.simulate(T, S, 1, K=K, coverage=coverage, seed=data_seed, u=u, omega=0.9)
+    meth, tot = d["meth_control"], d["tot_control"]
+    if zero is not None:
+        meth[zero[0]:zero[1]] = 0
+        tot[zero[0]:zero[1]] = 0
+    P = np.full((K, K), 1.0 / (K - 1))
+    np.fill_diagonal(P, 0.0)
+    if omega is None:
+        omega = sb.DEFAULT_OMEGA if K == 6 else [0.95] * K
+    omega = np.asarray(omega, np.float64)
+    p = sb.make_params(K=K, mu=mu, sigma=sg, P=P, omega=omega, u=u, Nmax=Nmax, epsilon=epsilon)
+    E = sb.emission(p, meth, tot)
+    out = sb.chain(p, E, seed, chain_id)
+    assert out["status"] == 0
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), K=K, u=u, Nmax=Nmax, epsilon=epsilon,
+                        seed=np.uint64(seed), chain_id=np.uint64(chain_id), mu=mu, sigma=sg, P=P, omega=omega,
+                        meth=meth, tot=tot, regime=d["regime_control"], E=E, regime_probs=out["regime_probs"])
+
+
 def main():
-    for name, kw in CHAINS.items():
-        chain_fixture(name, **kw)
-    tables_fixture()
+    only_sg = "sg" in sys.argv[1:]
+    if not only_sg:
+        for name, kw in CHAINS.items():
+            chain_fixture(name, **kw)
+        tables_fixture()
+    for name, kw in SG_CHAINS.items():
+        sg_chain_fixture(name, **kw)
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

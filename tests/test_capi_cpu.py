@@ -115,3 +115,70 @@ def test_product_package_does_not_import_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.sub(r"(#|//).*", "", txt).replace("oracle/", ""), f
+
+
+# ------------------------------------------------------------ single group
+def _sg_params(**kw):
+    from oracle import sg_binding
+
+    return _lib.SgParams.from_buffer_copy(bytes(sg_binding.make_params(**kw)))
+
+
+def test_sg_struct_layout_matches_c():
+    from oracle import sg_binding
+
+    assert C.sizeof(_lib.SgParams) == sg_binding.lib().oracle_sizeof_sg_params()
+    assert C.sizeof(_lib.SgChain) == 40
+
+
+def test_sg_params_default_is_pipeline_config(lib):
+    p = _lib.SgParams()
+    lib.hyg_sg_params_default(C.byref(p))
+    assert (p.n_regimes, p.minimum_duration, p.num_particles_max, p.resample_type) == (6, 3, 250, 2)
+    assert p.epsilon == 0.01 and p.is_kappa_fixed == 1 and p.theta_len == 36
+    np.testing.assert_allclose(list(p.alpha[:6]), [17.1, 0.9, 12, 3, 12, 1], rtol=1e-6)
+    m = C.c_void_p()
+    assert lib.hyg_sg_model_create(C.byref(p), 100, 1000, C.byref(m)) == _lib.HYG_OK
+    lib.hyg_sg_model_destroy(m)
+
+
+def test_sg_model_create_and_workspace(lib):
+    m = C.c_void_p()
+    assert lib.hyg_sg_model_create(C.byref(_sg_params(K=6)), 100, 5000, C.byref(m)) == _lib.HYG_OK
+    try:
+        one = lib.hyg_sg_workspace_bytes(m, 1, 64)
+        assert one >= 64 * 6 * 256 * 8
+        assert lib.hyg_sg_workspace_bytes(m, 3, 64) >= 3 * one - 512
+        assert lib.hyg_sg_workspace_bytes(m, 1, 0) > lib.hyg_sg_workspace_bytes(m, 1, 64)
+    finally:
+        lib.hyg_sg_model_destroy(m)
+
+
+@pytest.mark.parametrize("field,value,code", [("n_regimes", 1, _lib.HYG_EINVAL), ("num_particles_max", 6, _lib.HYG_EINVAL),
+                                              ("num_particles_max", 300, _lib.HYG_EUNSUPPORTED),
+                                              ("resample_type", 1, _lib.HYG_EUNSUPPORTED),
+                                              ("minimum_duration", 0, _lib.HYG_EINVAL),
+                                              ("theta_len", 35, _lib.HYG_EINVAL), ("epsilon", 0.0, _lib.HYG_EINVAL)])
+def test_sg_model_create_rejects_invalid(lib, field, value, code):
+    p = _sg_params(K=6)
+    setattr(p, field, value)
+    m = C.c_void_p()
+    assert lib.hyg_sg_model_create(C.byref(p), 100, 1000, C.byref(m)) == code
+    assert lib.hyg_last_error()
+
+
+def test_sg_compute_refuses_without_device(lib):
+    if lib.hyg_device_count() > 0:
+        pytest.skip("host without a GPU only")
+    m = C.c_void_p()
+    assert lib.hyg_sg_model_create(C.byref(_sg_params(K=6)), 100, 1000, C.byref(m)) == _lib.HYG_OK
+    try:
+        T = 10
+        z = np.zeros((T, 2), np.uint16)
+        out = np.zeros((T, 6))
+        ptr = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        assert lib.hyg_sg_run_chain_host(m, ptr(z), ptr(z), 2, T, 0, 0, ptr(out)) == _lib.HYG_EDEVICE
+        assert b"no CPU fallback" in lib.hyg_last_error()
+        assert lib.hyg_sg_emission(m, ptr(z), ptr(z), 2, T, ptr(out), None) == _lib.HYG_EDEVICE
+    finally:
+        lib.hyg_sg_model_destroy(m)
