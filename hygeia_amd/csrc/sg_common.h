@@ -49,6 +49,6 @@ int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint1
                        int S, int64_t n_sites, double* E, void* stream);
 int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
                      const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream);
-size_t sg_lds_bytes(const hyg_sg_consts& c);
+size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap);
 
 }  // namespace hyg

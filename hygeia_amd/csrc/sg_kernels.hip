@@ -13,8 +13,10 @@
 // algorithms/OnlineCombinedInference.h:48-118, singleGroup.h:556-627.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "../../include/hyg_arith.h"
 #include "hyg_dev.h"
@@ -26,22 +28,22 @@ __device__ __forceinline__ uint32_t sg_pack(int d, int r) { return (uint32_t)d |
 __device__ __forceinline__ int sg_d(uint32_t s) { return (int)(s & 0xffffffu); }
 __device__ __forceinline__ int sg_r(uint32_t s) { return (int)(s >> 24); }
 
-// Model::evaluateLogTransitionDensity for (1, rc) or (dc > 1, rc == rp) from (dp, rp)
-__device__ __forceinline__ double sg_trans(const SgModelDev& md, const hyg_sg_consts& c, int dc, int rc, int dp,
-                                           int rp) {
-  int d = dp - 1;
-  if (d >= md.dcap) d = md.dcap - 1;
-  const double2 h = *(const double2*)(md.hz + ((size_t)rp * md.dcap + d) * 2);
-  if (dc == 1 && rc != rp && dp >= c.u) {
-    const double lp = c.logP[rp * c.K + rc];
-    return md.ex[(size_t)rp * md.dcap + d] ? lp : (h.x + lp);
-  }
-  if (dc > 1 && rc == rp) return h.y;
-  return HYG_NINF;
+// Model::evaluateLogTransitionDensity (singleGroup.h:569-608) split per
+// previous particle (d, r): the density of a fresh particle (1, q) is
+// base + log P[r][q] with base = log rho(d, r) (0 after the hazard's exit, -inf
+// for d < u), and of the continuing particle (d + 1, r) it is cont =
+// log(1 - rho(d, r)). Both equal the oracle's sg_trans bit for bit (the
+// diagonal log P[r][r] = -inf covers q == r).
+__device__ __forceinline__ void sg_trans_parts(const SgModelDev& md, int u, uint32_t s, double& base,
+                                               double& cont) {
+  const int d = sg_d(s), r = sg_r(s);
+  int di = d - 1;
+  if (di >= md.dcap) di = md.dcap - 1;
+  const double2 h = *(const double2*)(md.hz + ((size_t)r * md.dcap + di) * 2);
+  const uint8_t ex = md.ex[(size_t)r * md.dcap + di];
+  base = (d >= u) ? (ex ? 0.0 : h.x) : HYG_NINF;
+  cont = h.y;
 }
-
-// exact wave sum of u128 values (all 64 lanes active)
-__device__ __forceinline__ double wave_fixsum(hyg_u128 v) { return hyg_u128_to_f64(wave_sum128(v), 100); }
 
 // ceil(T * R) for a double T in [0, 1] and R < 2^127 (oracle/sg_oracle.c:ceil_mul_f64)
 __device__ __forceinline__ hyg_u128 sg_ceil_mul_f64(double T, hyg_u128 R) {
@@ -73,41 +75,65 @@ __device__ __forceinline__ hyg_u128 sg_ceil_mul_f64(double T, hyg_u128 R) {
 }
 
 
+
 // ------------------------------------------------------------ LDS layout
+constexpr int kSgChunk = 32;  // pending entries finalised per smoothing round
+
 struct SgShared {
   int npend, nfree, cur, status;
+  int Kk, pad0;
+  unsigned int lmask;  // free psi slots resident in LDS
+  int pad1;
+  double logC;
+  unsigned long long ph[16];  // phase timers (diagnostic runs only)
 };
 
 struct SgLay {
-  size_t stP, stC, lwP, lwC, wP, wC, lwres, anc, idx, cum, BK, scr, mean, red, sh, total;
+  size_t st, lw, w, base, cont;  // [2][NT]: current / previous particle sets, alternating per step
+  size_t anc, lwres, logq, sidx, cum, xk, xi, BK, logP, red, lsev, scr, meanb, okb, logm, logQ, psil, sh, total;
+  int nl;  // psi slots resident in LDS (slot ids 0 .. nl-1; the rest live in the workspace)
 };
 
 __host__ __device__ inline size_t sg_align(size_t x) { return (x + 15) / 16 * 16; }
 
-__host__ __device__ inline SgLay sg_layout(int K) {
+__host__ __device__ inline SgLay sg_layout(int K, int cap) {
   SgLay l{};
   const int NT = kSgThreads, NW = NT / 64;
   size_t o = 0;
-  l.stP = o; o = sg_align(o + 4 * NT);
-  l.stC = o; o = sg_align(o + 4 * NT);
-  l.lwP = o; o = sg_align(o + 8 * NT);
-  l.lwC = o; o = sg_align(o + 8 * NT);
-  l.wP = o; o = sg_align(o + 8 * NT);
-  l.wC = o; o = sg_align(o + 8 * NT);
-  l.lwres = o; o = sg_align(o + 8 * NT);
+  l.st = o; o = sg_align(o + 4 * 2 * NT);
+  l.lw = o; o = sg_align(o + 8 * 2 * NT);
+  l.w = o; o = sg_align(o + 8 * 2 * NT);
+  l.base = o; o = sg_align(o + 8 * 2 * NT);
+  l.cont = o; o = sg_align(o + 8 * 2 * NT);
   l.anc = o; o = sg_align(o + 4 * NT);
-  l.idx = o; o = sg_align(o + 4 * NT);
+  l.lwres = o; o = sg_align(o + 8 * NT);
+  l.logq = o; o = sg_align(o + 8 * NT);
+  l.sidx = o; o = sg_align(o + 4 * NT);
   l.cum = o; o = sg_align(o + 16 * (NT + 1));
+  l.xk = o; o = sg_align(o + 8 * 2 * NT);
+  l.xi = o; o = sg_align(o + 4 * 2 * NT);
   l.BK = o; o = sg_align(o + 8 * (size_t)K * NT);
+  l.logP = o; o = sg_align(o + 8 * (size_t)K * K);
+  l.red = o; o = sg_align(o + 24 * (size_t)NW * K + 64);
+  l.lsev = o; o = sg_align(o + 8 * 2 * (size_t)K);
   l.scr = o; o = sg_align(o + 8 * (size_t)NW * NT);
-  l.mean = o; o = sg_align(o + 8 * (size_t)NW * HYG_KMAX);
-  l.red = o; o = sg_align(o + 16 * NW);
+  l.meanb = o; o = sg_align(o + 8 * (size_t)kSgChunk * K);
+  l.okb = o; o = sg_align(o + (size_t)kSgChunk * K);
+  l.logm = o; o = sg_align(o + 8 * (NT + 1));
+  l.logQ = o; o = sg_align(o + 8 * (NT + 1));
   l.sh = o; o = sg_align(o + sizeof(SgShared));
+  const size_t slot = 8 * (size_t)K * NT;
+  const size_t budget = 160 * 1024;
+  int nl = o < budget ? (int)((budget - o) / slot) : 0;
+  if (nl > 32) nl = 32;
+  if (nl > cap) nl = cap;
+  l.nl = nl;
+  l.psil = o; o = sg_align(o + slot * nl);
   l.total = o;
   return l;
 }
 
-size_t sg_lds_bytes(const hyg_sg_consts& c) { return sg_layout(c.K).total; }
+size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap) { return sg_layout(c.K, psi_cap).total; }
 
 // ------------------------------------------------------------- emission
 // E[t][r] = sum_s log BB(y_ts | n_ts, alpha_r, beta_r) in the oracle's term
@@ -144,129 +170,200 @@ sg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
   }
 }
 
+
 // --------------------------------------------------------- chain kernel
-// Block-wide exact log-sum-exp (thread n holds x_n, -inf when unused).
-__device__ __forceinline__ double sg_block_lse(double x, unsigned char* red) {
-  const double mx = block_max<kSgThreads>(x, red);
-  if (!(mx > HYG_NINF)) return HYG_NINF;
-  const hyg_u128 s = block_sum128<kSgThreads>(hyg_fix100(hyg_exp(x - mx)), red);
-  return mx + hyg_log(hyg_u128_to_f64(s, 100));
+// order key of a double: ascending key == ascending value (-0.0 == +0.0)
+__device__ __forceinline__ uint64_t sg_okey(double x) {
+  uint64_t b = u_of(x);
+  if (b == 0x8000000000000000ull) b = 0;
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
-// Wave-level exact log-sum-exp over the 4 values per lane (n = lane + 64 i)
-__device__ __forceinline__ double sg_wave_lse4(const double v[4]) {
-  double mx = dmax(dmax(v[0], v[1]), dmax(v[2], v[3]));
-  mx = wave_max(mx);
-  if (!(mx > HYG_NINF)) return HYG_NINF;
-  hyg_u128 s = hyg_u128_zero();
+__device__ __forceinline__ double sg_okey_value(uint64_t k) {
+  return d_of((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k);
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)v, m), hi = __shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+// Bitonic sort of the NT (key, idx) pairs held one per thread into descending
+// key, ties by ascending idx (the order of arma::sort_index "descend" /
+// oracle sort_desc); afterwards thread q holds the element of sorted position
+// q. Distances < 64 exchange through lane shuffles, 64 and 128 through LDS
+// (xk / xi, two buffers so consecutive cross-wave steps need one barrier each).
+__device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk, int* xi) {
+  constexpr int NT = kSgThreads;
+  const int tid = threadIdx.x;
+  int buf = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) s = hyg_u128_add(s, hyg_fix100(hyg_exp(v[i] - mx)));
-  return mx + hyg_log(hyg_u128_to_f64(wave_sum128(s), 100));
+  for (int k = 2; k <= NT; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint64_t pk;
+      int pi;
+      if (j >= 64) {
+        xk[buf * NT + tid] = key;
+        xi[buf * NT + tid] = idx;
+        lds_barrier();
+        pk = xk[buf * NT + (tid ^ j)];
+        pi = xi[buf * NT + (tid ^ j)];
+        buf ^= 1;
+      } else {
+        pk = shfl_xor64(key, j);
+        pi = __shfl_xor(idx, j);
+      }
+      const bool up = (tid & k) == 0, lower = (tid & j) == 0;
+      const bool pfirst = pk > key || (pk == key && pi < idx);
+      if ((lower == up) ? pfirst : !pfirst) {
+        key = pk;
+        idx = pi;
+      }
+    }
+  }
 }
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
-// sorted position of value v of thread `me` among vals[0, n): descending, ties by index
-__device__ __forceinline__ int sg_rank_desc(const double* vals, int n, double v, int me) {
-  int rank = 0;
-  for (int m = 0; m < n; ++m) {
-    const double w = vals[m];
-    rank += (w > v || (w == v && m < me)) ? 1 : 0;
-  }
-  return rank;
-}
 
-// One workgroup per chain, thread n = particle n. The pending smoothing times
-// live in the chain's workspace region: cap slots of psi [K][256] doubles and
-// the lists slot[2][cap], time[2][cap], keep[cap], free[cap] (int32).
+// One workgroup per chain, thread n = particle n (N_max <= 256). Per step the
+// critical path is a few dozen barriers: sorts in registers, the K / log c
+// fixed point in one wave, batched reductions for the K fresh-particle rows
+// and backward kernels, and the smoothing split into (pending time, regime)
+// tasks over all waves with the psi rows resident in LDS (up to 32 slots,
+// the rest in the chain's workspace region).
+template <int KT>
 __global__ void __launch_bounds__(kSgThreads)
 sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const double* __restrict__ E,
                 uint8_t* __restrict__ ws, int cap, double* __restrict__ probs, int32_t* __restrict__ status_out,
-                SgLay lay) {
-  constexpr int NT = kSgThreads, NW = NT / 64;
+                SgLay lay, unsigned long long* __restrict__ dbg) {
+  constexpr int NT = kSgThreads, NW = NT / 64, K = KT;
   const hyg_sg_consts& c = *md.consts;
-  const int K = c.K, Nmax = c.Nmax, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int Nmax = c.Nmax, u = c.u, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const double eps = c.epsilon;
   const SgChainDev ch = chains[blockIdx.x];
   const int T = ch.T;
   extern __shared__ __align__(16) unsigned char smem[];
-  uint32_t* stP = (uint32_t*)(smem + lay.stP);
-  uint32_t* stC = (uint32_t*)(smem + lay.stC);
-  double* lwP = (double*)(smem + lay.lwP);
-  double* lwC = (double*)(smem + lay.lwC);
-  double* wP = (double*)(smem + lay.wP);
-  double* wC = (double*)(smem + lay.wC);
-  double* lwres = (double*)(smem + lay.lwres);
+  uint32_t* st_ = (uint32_t*)(smem + lay.st);
+  double* lw_ = (double*)(smem + lay.lw);
+  double* w_ = (double*)(smem + lay.w);
+  double* base_ = (double*)(smem + lay.base);
+  double* cont_ = (double*)(smem + lay.cont);
   int* anc = (int*)(smem + lay.anc);
-  int* idx = (int*)(smem + lay.idx);
+  double* lwres = (double*)(smem + lay.lwres);
+  double* logq = (double*)(smem + lay.logq);
+  int* sidx = (int*)(smem + lay.sidx);
   hyg_u128* cum = (hyg_u128*)(smem + lay.cum);
+  uint64_t* xk = (uint64_t*)(smem + lay.xk);
+  int* xi = (int*)(smem + lay.xi);
   double* BK = (double*)(smem + lay.BK);
-  double* scr = (double*)(smem + lay.scr) + wv * NT;
-  double* meanb = (double*)(smem + lay.mean) + wv * HYG_KMAX;
+  double* logP = (double*)(smem + lay.logP);
   unsigned char* red = smem + lay.red;
+  double* lsev = (double*)(smem + lay.lsev);
+  double* scr = (double*)(smem + lay.scr) + wv * NT;
+  double* meanb = (double*)(smem + lay.meanb);
+  uint8_t* okb = smem + lay.okb;
+  double* psil = (double*)(smem + lay.psil);
+  double* logm = (double*)(smem + lay.logm);
+  double* logQ = (double*)(smem + lay.logQ);
   SgShared& sh = *(SgShared*)(smem + lay.sh);
-  uint8_t* base = ws + ch.psi_offset;
-  double* psi = (double*)base;
-  int32_t* lists = (int32_t*)(base + sg_psi_region_bytes(K, cap));
+  const int nl = lay.nl;
+  uint8_t* wbase = ws + ch.psi_offset;
+  double* psig = (double*)wbase;
+  int32_t* lists = (int32_t*)(wbase + sg_psi_region_bytes(K, cap));
   int32_t* keepf = lists + 4 * (size_t)cap;
   int32_t* freel = lists + 5 * (size_t)cap;
   double* out = probs + (size_t)ch.out_begin * K;
   const double* Ech = E + (size_t)ch.site_begin * K;
+  auto slot_row = [&](int slot, int r) -> double* {
+    return slot < nl ? psil + ((size_t)slot * K + r) * NT : psig + ((size_t)(slot - nl) * K + r) * NT;
+  };
 
   for (int i = tid; i < cap; i += NT) freel[i] = cap - 1 - i;
+  for (int i = tid; i < K * K; i += NT) logP[i] = c.logP[i];
+  for (int i = tid; i <= NT; i += NT) logm[i] = hyg_log((double)i);  // log(M - k) of the K loop
+  // phase timers: 0 copy, 1 sort, 2 K loop, 3 residual / keep-top, 4 weights,
+  // 5 normalise, 6 smoothing, 7 compaction; counters 8 optimal steps, 9
+  // keep-top steps, 10 K-loop iterations, 11 pending entries, 15 = last stamp
+  if (tid < 16) sh.ph[tid] = 0;
+#define SG_PH(k)                                                   \
+  if (dbg && tid == 0) {                                           \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    sh.ph[k] += now_ - sh.ph[15];                                  \
+    sh.ph[15] = now_;                                              \
+  }
+#define SG_CNT(k, v) \
+  if (dbg && tid == 0) sh.ph[k] += (v);
   if (tid == 0) {
     sh.npend = 0;
     sh.nfree = cap;
     sh.cur = 0;
     sh.status = HYG_OK;
+    sh.lmask = nl >= 32 ? 0xffffffffu : ((1u << nl) - 1u);
   }
   // ---- t = 0 (Smc.h:114-188): N = K particles (1, r), log w = -log K + log g_0(r)
   int N = K;
-  double x = HYG_NINF;
-  if (tid < K) {
-    stC[tid] = sg_pack(1, tid);
-    x = -c.log_K + Ech[tid];
-    lwC[tid] = x;
-  }
-  double logZ = sg_block_lse(x, red);
-  if (!(logZ > HYG_NINF)) {
+  uint32_t my_st = sg_pack(1, tid < K ? tid : 0);
+  double my_lw = (tid < K) ? -c.log_K + Ech[tid] : HYG_NINF;
+  double my_base = HYG_NINF, my_cont = HYG_NINF;
+  if (tid < K) sg_trans_parts(md, u, my_st, my_base, my_cont);
+  double mx0;
+  int fin;
+  block_max_cnt<NT>(my_lw, (tid < K && hyg_isfinite(my_lw)) ? 1 : 0, red, &mx0, &fin);
+  if (!(mx0 > HYG_NINF)) {
     if (tid == 0) status_out[blockIdx.x] = HYG_ENUMERIC;
     return;
   }
-  if (tid < K) wC[tid] = hyg_exp(lwC[tid] - logZ);
+  double logZ =
+      mx0 + hyg_log(hyg_u128_to_f64(block_sum128<NT>(hyg_fix100(hyg_exp(my_lw - mx0)), red), 100));
+  double my_w = (tid < K) ? hyg_exp(my_lw - logZ) : 0.0;
+  if (tid < K) {
+    st_[tid] = my_st;
+    lw_[tid] = my_lw;
+    w_[tid] = my_w;
+    base_[tid] = my_base;
+    cont_[tid] = my_cont;
+  }
   __syncthreads();
 
   int status = HYG_OK;
+  if (dbg && tid == 0) sh.ph[15] = __builtin_amdgcn_s_memtime();
   for (int t = 0; t < T; ++t) {
     const bool final = (t == T - 1);
+    const int cb = t & 1, pb = cb ^ 1;  // LDS buffers of the current / previous particle sets
     int M = 0, Np = N;
     if (t > 0) {
-      // ---- Smc::iterate (:190-286): previous <- current
-      if (tid < Np) {
-        stP[tid] = stC[tid];
-        lwP[tid] = lwC[tid];
-        wP[tid] = wC[tid];
-      }
+      // ---- Smc::iterate (:190-286): the current set becomes the previous one
+      const uint32_t* stP = st_ + pb * NT;
+      const double* lwP = lw_ + pb * NT;
+      const double* contP = cont_ + pb * NT;
+      const double* Et = Ech + (size_t)t * K;
+      double et[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) et[q] = Et[q];
       const double logZp = logZ;
+      const double pw = my_w, plw = my_lw, pbase = my_base;
+      const uint32_t pst = my_st;
       N = (Np + K > Nmax) ? Nmax : Np + K;
       M = N - K;
-      lds_barrier();
+      SG_PH(0);
       // ---- resampleCp (:406-450)
       if (N < Np + K) {
-        int fin;
-        (void)block_excl_int<NT>((tid < Np && hyg_isfinite(lwP[tid])) ? 1 : 0, red, &fin);
         bool keep_top = true;
         if (fin > M) {
           // optimalFiniteState (resample.h:289-409) on the sorted self-normalised weights
-          if (tid < Np) idx[sg_rank_desc(wP, Np, wP[tid], tid)] = tid;
-          lds_barrier();
+          uint64_t key = (tid < Np) ? sg_okey(pw) : 0;
+          int idx = tid;
+          sg_bitonic(key, idx, xk, xi);
           double lq = HYG_NINF;
           hyg_u128 mq = hyg_u128_zero();
           if (tid < Np) {
-            const double q = wP[idx[tid]];
+            const double q = sg_okey_value(key);
             lq = hyg_log(q);
             mq = hyg_fix100(q);
           }
+          logq[tid] = lq;
+          sidx[tid] = idx;
           // reverse cumulative sums Q(k) = total - exclusive prefix (exact)
           block_scan128<NT>(mq, cum, red);
           lds_barrier();
@@ -277,35 +374,59 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
             suf.hi = tot.hi - ex.hi - (tot.lo < ex.lo ? 1u : 0u);
             lds_barrier();
             cum[tid] = suf;
-            if (tid == 0) cum[NT] = hyg_u128_zero();
+            logQ[tid] = hyg_log(hyg_u128_to_f64(suf, 100));
+            if (tid == 0) {
+              cum[NT] = hyg_u128_zero();
+              logQ[NT] = HYG_NINF;
+            }
           }
           lds_barrier();
-          // the K / log c fixed point (:333-342), counts block-parallel
-          int kOld = 1, kNew = 0;
-          double logC = 0.0;
-          while (kNew != kOld) {
-            kOld = kNew;
-            const double Qk = hyg_u128_to_f64(cum[kOld], 100);
-            logC = hyg_log((double)(M - kOld)) - hyg_log(Qk);
-            int cnt;
-            (void)block_excl_int<NT>((tid >= kOld && tid < Np && lq > -logC) ? 1 : 0, red, &cnt);
-            kNew = kOld + cnt;
+          SG_PH(1);
+          // the K / log c fixed point (:333-342) in wave 0: counts by ballot
+          if (wv == 0) {
+            double lq4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lq4[i] = logq[lane + 64 * i];
+            int kOld = 1, kNew = 0, iters = 0;
+            double logC = 0.0;
+            while (kNew != kOld) {
+              kOld = kNew;
+              // hyg_log(M - kOld) - hyg_log(Q(kOld)) from the tables (log of a negative count is NaN)
+              const int mk = M - kOld;
+              logC = (mk >= 0 ? logm[mk] : HYG_NAN) - logQ[kOld];
+              const double thr = -logC;
+              int cnt = 0;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int p = lane + 64 * i;
+                cnt += __builtin_popcountll(__ballot(p >= kOld && p < Np && lq4[i] > thr));
+              }
+              kNew = kOld + cnt;
+              ++iters;
+            }
+            if (lane == 0) {
+              sh.Kk = kNew;
+              sh.logC = logC;
+            }
+            SG_CNT(10, iters);
           }
+          lds_barrier();
+          SG_PH(2);
+          const double logC = sh.logC;
           if (hyg_isfinite(logC)) {
             keep_top = false;
-            const int Kk = kNew, L = M - Kk;
+            const int Kk = sh.Kk, L = M - Kk;
             if (tid < Kk) {
-              anc[tid] = idx[tid];
-              lwres[tid] = lwP[idx[tid]];
+              anc[tid] = idx;
+              lwres[tid] = lwP[idx];
             }
             if (L > 0) {
               // residual systematic draw (:372-377, systematicBase :85-117):
               // T_j = (j + u) / L <= Q_i as exact C_i >= ceil(T_j R)
-              const double rv = (tid >= Kk && tid < Np) ? lq : HYG_NINF;
-              const double rmax = block_max<NT>(rv, red);
-              hyg_u128 m2 = hyg_u128_zero();
-              if (tid >= Kk && tid < Np) m2 = hyg_fix100(hyg_exp(lq - rmax));
-              block_scan128<NT>(m2, cum, red);  // also a barrier before the overwrite
+              const bool inres = tid >= Kk && tid < Np;
+              const double rmax = block_max<NT>(inres ? lq : HYG_NINF, red);
+              const hyg_u128 m2 = inres ? hyg_fix100(hyg_exp(lq - rmax)) : hyg_u128_zero();
+              block_scan128<NT>(m2, cum, red);
               const hyg_u128 incl = hyg_u128_add(cum[tid], m2);
               lds_barrier();
               cum[tid] = incl;
@@ -322,7 +443,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
                   const int mid = (lo + hi) >> 1;
                   if (hyg_u128_lt(cum[mid], thr)) lo = mid + 1; else hi = mid;
                 }
-                anc[Kk + tid] = idx[lo];
+                anc[Kk + tid] = sidx[lo];
                 lwres[Kk + tid] = logZp - logC;
               }
             }
@@ -330,77 +451,143 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         }
         if (keep_top) {
           // keep the M largest log-weights (Smc.h:432-441, resample.h:379-384)
-          if (tid < Np) {
-            const double v = lwP[tid];
-            const int rank = sg_rank_desc(lwP, Np, v, tid);
-            if (rank < M) {
-              anc[rank] = tid;
-              lwres[rank] = v;
-            }
+          uint64_t key = (tid < Np) ? sg_okey(plw) : 0;
+          int idx = tid;
+          sg_bitonic(key, idx, xk, xi);
+          if (tid < M) {
+            anc[tid] = idx;
+            lwres[tid] = lwP[idx];
           }
         }
+        SG_CNT(8, keep_top ? 0 : 1);
+        SG_CNT(9, keep_top ? 1 : 0);
       } else if (tid < M) {
         anc[tid] = tid;
-        lwres[tid] = lwP[tid];
+        lwres[tid] = plw;
       }
       lds_barrier();
+      SG_PH(3);
       // ---- sampleParticlesCp (:504-522) + computeWeightsCp (:536-574)
-      const double* Et = Ech + (size_t)t * K;
+      double nlw = HYG_NINF;
+      uint32_t nst = 0;
       if (tid < M) {
-        const uint32_t a = stP[anc[tid]];
-        const int d = sg_d(a) + 1, r = sg_r(a);
-        stC[tid] = sg_pack(d, r);
-        lwC[tid] = lwres[tid] + (sg_trans(md, c, d, r, sg_d(a), r) + Et[r]);
+        const int a = anc[tid];
+        const uint32_t sa = stP[a];
+        const int r = sg_r(sa);
+        double e = et[0];
+#pragma unroll
+        for (int q = 1; q < K; ++q) e = (r == q) ? et[q] : e;
+        nst = sg_pack(sg_d(sa) + 1, r);
+        nlw = lwres[tid] + (contP[a] + e);
       }
-      // new particles (1, q) and the backward kernels (:288-326), one row q per wave
-      for (int q = wv; q < K; q += NW) {
-        const double eq = Et[q];
-        double vn[4], vb[4];
+      // backward kernels (:288-326) K_q(n) = exp(x_qn - max_q) / S_q with
+      // x_qn = W_prev[n] + log f((1,q) | n), and the fresh particles (1, q) with
+      // log weight max_q + log S_q + log g_t(q): thread n = previous particle n,
+      // the K row reductions batched (oracle/sg_oracle.c)
+      double vb[K];
+      {
+        const bool live = tid < Np;
+        const int rp = sg_r(pst);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = lane + 64 * i;
-          vn[i] = HYG_NINF;
-          vb[i] = HYG_NINF;
-          if (n < Np) {
-            const uint32_t s = stP[n];
-            const double tr = sg_trans(md, c, 1, q, sg_d(s), sg_r(s));
-            vn[i] = (tr + eq) + lwP[n];
-            vb[i] = lwP[n] + tr;
-          }
+        for (int q = 0; q < K; ++q) vb[q] = live ? plw + (pbase + logP[rp * K + q]) : HYG_NINF;
+      }
+      double* redd = (double*)red;
+      hyg_u128* redu = (hyg_u128*)(red + 8 * NW * K);
+      double mq[K];
+#pragma unroll
+      for (int q = 0; q < K; ++q) mq[q] = wave_max(vb[q]);
+      if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) redd[wv * K + q] = mq[q];
+      }
+      lds_barrier();
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        double m = redd[q];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) m = dmax(m, redd[w * K + q]);
+        mq[q] = m;
+      }
+      double ev[K];
+      {
+        hyg_u128 s2[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          ev[q] = hyg_exp(vb[q] - mq[q]);
+          s2[q] = hyg_fix100(ev[q]);
         }
-        const double ln = sg_wave_lse4(vn);
-        const double lb = sg_wave_lse4(vb);
+#pragma unroll
+        for (int q = 0; q < K; ++q) s2[q] = wave_sum128(s2[q]);
         if (lane == 0) {
-          lwC[M + q] = ln;
-          stC[M + q] = sg_pack(1, q);
-        }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = lane + 64 * i;
-          if (n < Np) BK[q * NT + n] = (lb > HYG_NINF) ? hyg_exp(vb[i] - lb) : 0.0;
+          for (int q = 0; q < K; ++q) redu[wv * K + q] = s2[q];
         }
       }
       lds_barrier();
+      if (tid < K) {
+        double m = HYG_NINF;
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+          if (q == tid) m = mq[q];
+        hyg_u128 s = hyg_u128_zero();
+        for (int w = 0; w < NW; ++w) s = hyg_u128_add(s, redu[w * K + tid]);
+        const double S = hyg_u128_to_f64(s, 100);
+        lsev[tid] = (m > HYG_NINF) ? m + hyg_log(S) : HYG_NINF;  // log-normaliser of row q
+        lsev[K + tid] = (m > HYG_NINF) ? 1.0 / S : 0.0;
+      }
+      lds_barrier();
+      if (tid < Np) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) BK[q * NT + tid] = (lsev[q] > HYG_NINF) ? ev[q] * lsev[K + q] : 0.0;
+      }
+      if (tid >= M && tid < N) {
+        const int q = tid - M;
+        double e = et[0];
+#pragma unroll
+        for (int qq = 1; qq < K; ++qq) e = (q == qq) ? et[qq] : e;
+        const double lb = lsev[q];
+        nlw = (lb > HYG_NINF) ? lb + e : HYG_NINF;
+        nst = sg_pack(1, q);
+      }
+      SG_PH(4);
       // ---- selfNormaliseWeights (:576-579)
-      logZ = sg_block_lse(tid < N ? lwC[tid] : HYG_NINF, red);
-      if (!(logZ > HYG_NINF)) {
+      double mx;
+      block_max_cnt<NT>(nlw, (tid < N && hyg_isfinite(nlw)) ? 1 : 0, red, &mx, &fin);
+      if (!(mx > HYG_NINF)) {
         status = HYG_ENUMERIC;
         break;
       }
-      if (tid < N) wC[tid] = hyg_exp(lwC[tid] - logZ);
+      logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NT>(hyg_fix100(hyg_exp(nlw - mx)), red), 100));
+      my_lw = nlw;
+      my_st = nst;
+      my_w = (tid < N) ? hyg_exp(nlw - logZ) : 0.0;
+      if (tid < N) {
+        st_[cb * NT + tid] = my_st;
+        lw_[cb * NT + tid] = my_lw;
+        w_[cb * NT + tid] = my_w;
+        sg_trans_parts(md, u, my_st, my_base, my_cont);  // consumed next step
+      }
+      SG_PH(5);
     }
     // ---- online marginal smoothing: updatePsi (OnlineMarginalSmoothing.h:152-197)
     //      of the pending times, initialisePsi (:132-150) of time t, storeEstimates
-    //      (:199-253) with the epsilon rule
+    //      (:199-253) with the epsilon rule, as (pending time, regime) tasks
     const int cur = sh.cur, nold = sh.npend;
     int32_t* slotA = lists + (size_t)cur * 2 * cap;
     int32_t* timeA = slotA + cap;
     if (tid == 0) {
-      if (sh.nfree == 0) {
+      int slot = -1;
+      if (sh.lmask) {
+        const int b = __builtin_ctz(sh.lmask);
+        sh.lmask &= ~(1u << b);
+        slot = b;
+      } else if (sh.nfree > 0) {
+        slot = nl + freel[--sh.nfree];
+      }
+      if (slot < 0) {
         sh.status = HYG_ENOMEM;
       } else {
-        const int f = --sh.nfree;
-        slotA[nold] = freel[f];
+        slotA[nold] = slot;
         timeA[nold] = t;
       }
     }
@@ -409,13 +596,16 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       status = sh.status;
       break;
     }
+    const uint32_t* stC = st_ + cb * NT;
+    const double* wC = w_ + cb * NT;
     const int ntot = nold + 1;
-    for (int e = wv; e < ntot; e += NW) {
-      const bool fresh = (e == nold);
-      double* sp = psi + (size_t)slotA[e] * K * NT;
-      bool ok = true;
-      for (int r = 0; r < K; ++r) {
-        double* row = sp + (size_t)r * NT;
+    SG_CNT(11, ntot);
+    for (int c0 = 0; c0 < ntot; c0 += kSgChunk) {
+      const int ne = (ntot - c0 < kSgChunk) ? ntot - c0 : kSgChunk;
+      for (int task = wv; task < ne * K; task += NW) {
+        const int el = task / K, r = task - el * K, e = c0 + el;
+        const bool fresh = (e == nold);
+        double* row = slot_row(slotA[e], r);
         double nv[4];
         if (fresh) {
 #pragma unroll
@@ -429,22 +619,30 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           for (int i = 0; i < 4; ++i) {
             const int n = lane + 64 * i;
             pv[i] = (n < Np) ? row[n] : 0.0;
-            scr[n] = pv[i];
           }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) scr[lane + 64 * i] = pv[i];
           wave_lds_sync();
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int n = lane + 64 * i;
             nv[i] = (n < M) ? scr[anc[n]] : 0.0;
           }
+          hyg_u128 s[K];
+#pragma unroll
           for (int q = 0; q < K; ++q) {
-            hyg_u128 s = hyg_u128_zero();
+            s[q] = hyg_u128_zero();
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int n = lane + 64 * i;
-              if (n < Np) s = hyg_u128_add(s, hyg_fix100(BK[q * NT + n] * pv[i]));
+              if (n < Np) s[q] = hyg_u128_add(s[q], hyg_fix100(BK[q * NT + n] * pv[i]));
             }
-            const double v = hyg_u128_to_f64(wave_sum128(s), 100);
+          }
+#pragma unroll
+          for (int q = 0; q < K; ++q) s[q] = wave_sum128(s[q]);
+#pragma unroll
+          for (int q = 0; q < K; ++q) {
+            const double v = hyg_u128_to_f64(s[q], 100);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
               if (lane + 64 * i == M + q) nv[i] = v;
@@ -456,53 +654,73 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           const int n = lane + 64 * i;
           if (n < N) row[n] = nv[i];
         }
+        double wn[4];
         hyg_u128 sm = hyg_u128_zero();
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int n = lane + 64 * i;
-          if (n < N) sm = hyg_u128_add(sm, hyg_fix100(wC[n] * nv[i]));
+          wn[i] = (n < N) ? wC[n] : 0.0;
+          if (n < N) sm = hyg_u128_add(sm, hyg_fix100(wn[i] * nv[i]));
         }
         const double mean = hyg_u128_to_f64(wave_sum128(sm), 100);
-        if (lane == 0) meanb[r] = mean;
-        if (!final && ok) {
+        bool ok = true;
+        if (!final) {
           hyg_u128 sv = hyg_u128_zero();
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int n = lane + 64 * i;
             if (n < N) {
               const double dv = nv[i] - mean;
-              sv = hyg_u128_add(sv, hyg_fix100(wC[n] * (dv * dv)));
+              sv = hyg_u128_add(sv, hyg_fix100(wn[i] * (dv * dv)));
             }
           }
-          if (!(hyg_u128_to_f64(wave_sum128(sv), 100) < c.epsilon)) ok = false;
+          ok = hyg_u128_to_f64(wave_sum128(sv), 100) < eps;
+        }
+        if (lane == 0) {
+          meanb[el * K + r] = mean;
+          okb[el * K + r] = ok ? 1 : 0;
         }
       }
-      const bool store = final || ok;
-      wave_lds_sync();
-      if (store && lane < K) out[(size_t)timeA[e] * K + lane] = meanb[lane];
-      if (lane == 0) keepf[e] = store ? 0 : 1;
-      wave_lds_sync();
+      __syncthreads();
+      if (tid < ne) {
+        const int e = c0 + tid;
+        bool ok = true;
+#pragma unroll
+        for (int r = 0; r < K; ++r) ok = ok && okb[tid * K + r];
+        const bool store = final || ok;
+        if (store) {
+          double* o = out + (size_t)timeA[e] * K;
+#pragma unroll
+          for (int r = 0; r < K; ++r) o[r] = meanb[tid * K + r];
+        }
+        keepf[e] = store ? 0 : 1;
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    SG_PH(6);
     // compaction of the pending list into the other buffer; freed slots go
-    // back on the free list (the order of pending times does not matter)
+    // back to the LDS mask or the workspace free list (order is immaterial)
     {
       int32_t* slotB = lists + (size_t)(cur ^ 1) * 2 * cap;
       int32_t* timeB = slotB + cap;
       int nk = 0, nf = sh.nfree;
       for (int b = 0; b < ntot; b += NT) {
         const int e = b + tid;
-        const int kp = (e < ntot) ? keepf[e] : 0;
-        const int v = (e < ntot) ? (kp ? 1 : 0x10000) : 0;
+        const bool in = e < ntot;
+        const int kp = in ? keepf[e] : 0;
+        const int sl = in ? slotA[e] : 0;
+        const int v = in ? (kp ? 1 : (sl >= nl ? 0x10000 : 0)) : 0;
         int tot;
         const int ex = block_excl_int<NT>(v, red, &tot);
-        if (e < ntot) {
+        if (in) {
           if (kp) {
             const int p = nk + (ex & 0xffff);
-            slotB[p] = slotA[e];
+            slotB[p] = sl;
             timeB[p] = timeA[e];
+          } else if (sl >= nl) {
+            freel[nf + (ex >> 16)] = sl - nl;
           } else {
-            freel[nf + (ex >> 16)] = slotA[e];
+            atomicOr(&sh.lmask, 1u << sl);
           }
         }
         nk += tot & 0xffff;
@@ -514,12 +732,33 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         sh.nfree = nf;
         sh.cur = cur ^ 1;
       }
+      if (tid < N) {
+        base_[cb * NT + tid] = my_base;
+        cont_[cb * NT + tid] = my_cont;
+      }
       __syncthreads();
+      SG_PH(7);
     }
   }
   if (tid == 0) status_out[blockIdx.x] = status;
+  if (dbg && tid < 15) dbg[(size_t)blockIdx.x * 16 + tid] = sh.ph[tid];
+  if (dbg && tid == 15) dbg[(size_t)blockIdx.x * 16 + 15] = (unsigned long long)T;
+#undef SG_PH
+#undef SG_CNT
 }
 
+// ------------------------------------------------------------- launches
+template <int KT>
+static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, int n_chains, const double* E,
+                            uint8_t* ws, int cap, double* probs, int32_t* status, const SgLay& lay,
+                            unsigned long long* dbg, hipStream_t s, hipError_t* err) {
+  *err = hipFuncSetAttribute((const void*)sg_chain_kernel<KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lay.total);
+  if (*err != hipSuccess) return;
+  hipLaunchKernelGGL(sg_chain_kernel<KT>, dim3(n_chains), dim3(kSgThreads), lay.total, s, md, chains_dev, E, ws,
+                     cap, probs, status, lay, dbg);
+  *err = hipGetLastError();
+}
 // ------------------------------------------------------------- launches
 int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint16_t* meth, const uint16_t* tot,
                        int S, int64_t n_sites, double* E, void* stream) {
@@ -531,18 +770,57 @@ int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint1
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }
 
+
 int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
                      const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream) {
   if (n_chains <= 0) return HYG_OK;
-  if (c.Nmax > kSgThreads) return HYG_EUNSUPPORTED;
-  const SgLay lay = sg_layout(c.K);
+  if (c.Nmax > kSgThreads || c.K < 2 || c.K > HYG_KMAX) return HYG_EUNSUPPORTED;
+  const SgLay lay = sg_layout(c.K, psi_cap);
   if (lay.total > 160 * 1024) return HYG_EUNSUPPORTED;
-  if (hipFuncSetAttribute((const void*)sg_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lay.total) != hipSuccess)
+  static const bool want_dbg = getenv("HYG_SG_PHASES") != nullptr;
+  unsigned long long* dbg = nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  if (want_dbg && hipMalloc((void**)&dbg, sizeof(unsigned long long) * 16 * n_chains) != hipSuccess) dbg = nullptr;
+  if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * 16 * n_chains, s);
+  hipError_t err = hipErrorInvalidValue;
+  switch (c.K) {
+#define SG_CASE(k) \
+  case k: launch_chain_kt<k>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, dbg, s, &err); break;
+    SG_CASE(2) SG_CASE(3) SG_CASE(4) SG_CASE(5) SG_CASE(6) SG_CASE(7) SG_CASE(8) SG_CASE(9)
+    SG_CASE(10) SG_CASE(11) SG_CASE(12) SG_CASE(13) SG_CASE(14) SG_CASE(15) SG_CASE(16)
+#undef SG_CASE
+    default: break;
+  }
+  if (err != hipSuccess) {
+    if (dbg) (void)hipFree(dbg);
     return HYG_EDEVICE;
-  hipLaunchKernelGGL(sg_chain_kernel, dim3(n_chains), dim3(kSgThreads), lay.total, (hipStream_t)stream, md,
-                     chains_dev, E, ws, psi_cap, probs, status, lay);
-  return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
+  }
+  if (dbg) {
+    std::vector<unsigned long long> h((size_t)16 * n_chains);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
+    (void)hipFree(dbg);
+    // the longest chain (the critical path)
+    int lc = 0;
+    for (int i = 1; i < n_chains; ++i)
+      if (h[(size_t)i * 16 + 15] > h[(size_t)lc * 16 + 15]) lc = i;
+    const double steps = (double)h[(size_t)lc * 16 + 15];
+    const char* nm[8] = {"copy", "sort", "kloop", "resample", "weights", "normalise", "smooth", "compact"};
+    fprintf(stderr, "[hyg sg phases] K=%d lds=%zu slots_lds=%d longest chain %d: %.0f steps, cycles/step:", c.K,
+            lay.total, lay.nl, lc, steps);
+    double sum = 0;
+    for (int k = 0; k < 8; ++k) {
+      const double v = (double)h[(size_t)lc * 16 + k] / steps;
+      fprintf(stderr, " %s=%.0f", nm[k], v);
+      sum += v;
+    }
+    fprintf(stderr, " total=%.0f | optimal=%.0f keep_top=%.0f kloop_iters/capped=%.2f pending/step=%.2f\n", sum,
+            (double)h[(size_t)lc * 16 + 8], (double)h[(size_t)lc * 16 + 9],
+            (double)h[(size_t)lc * 16 + 10] /
+                std::max(1.0, (double)(h[(size_t)lc * 16 + 8] + h[(size_t)lc * 16 + 9])),
+            (double)h[(size_t)lc * 16 + 11] / steps);
+  }
+  return HYG_OK;
 }
 
 }  // namespace hyg

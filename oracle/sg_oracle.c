@@ -131,6 +131,10 @@ typedef struct {
   double* psi; /* [K][Nmax] */
 } pending_t;
 
+/* diagnostics: sum / max over steps of the number of pending smoothing times */
+int64_t oracle_sg_pending_sum = 0;
+int32_t oracle_sg_pending_max = 0;
+
 /* One chain over T sites: E [T][K] emission table. Writes probs [T][K]
  * (the smoothed regime probabilities). Returns HYG_OK / HYG_ENUMERIC / HYG_ENOMEM. */
 int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t seed, uint64_t chain_id,
@@ -275,22 +279,38 @@ int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t see
         rC[n] = rP[anc[n]];
         lwC[n] = lwres[n] + (sg_trans(&mo, dC[n], rC[n], dP[anc[n]], rP[anc[n]]) + Et[rC[n]]);
       }
+      /* evaluateBackwardKernels (:288-326): K_q(n) = normalise(W_prev[n] + log f((1,q) | n)),
+       * normalised as exp(x - max) / sum exp(x - max) (one reciprocal per row).
+       * The fresh particle (1, q) has log weight logsumexp_n(W_prev[n] + log f((1,q) | n))
+       * + log g_t(q): the reference's logsumexp_n(log f + log g + W_prev[n])
+       * (computeWeightsCp :563-573) with the n-independent log g taken out. */
       for (int q = 0; q < K; ++q) {
         dC[M + q] = 1;
         rC[M + q] = q;
-        for (int n = 0; n < Np; ++n) tmp[n] = (sg_trans(&mo, 1, q, dP[n], rP[n]) + Et[q]) + lwP[n];
-        lwC[M + q] = lse(tmp, Np);
+        double mx = -INFINITY;
+        for (int n = 0; n < Np; ++n) {
+          tmp[n] = lwP[n] + sg_trans(&mo, 1, q, dP[n], rP[n]);
+          if (tmp[n] > mx) mx = tmp[n];
+        }
+        if (mx > -INFINITY) {
+          hyg_u128 sacc = hyg_u128_zero();
+          for (int n = 0; n < Np; ++n) {
+            tmp2[n] = hyg_exp(tmp[n] - mx);
+            sacc = hyg_u128_add(sacc, hyg_fix100(tmp2[n]));
+          }
+          const double S = hyg_u128_to_f64(sacc, 100);
+          const double inv = 1.0 / S;
+          for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = tmp2[n] * inv;
+          lwC[M + q] = (mx + hyg_log(S)) + Et[q];
+        } else {
+          for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = 0.0;
+          lwC[M + q] = -INFINITY;
+        }
       }
       logZ = lse(lwC, N); /* selfNormaliseWeights (:576-579) */
       if (!(logZ > -INFINITY)) { rc = HYG_ENUMERIC; goto done; }
       for (int n = 0; n < N; ++n) wC[n] = hyg_exp(lwC[n] - logZ);
       if (nparts_out) nparts_out[t] = N;
-      /* evaluateBackwardKernels (:288-326): K_q(n) = normalise(W_prev[n] + log f((1,q) | n)) */
-      for (int q = 0; q < K; ++q) {
-        for (int n = 0; n < Np; ++n) tmp[n] = lwP[n] + sg_trans(&mo, 1, q, dP[n], rP[n]);
-        const double lz = lse(tmp, Np);
-        for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = (lz > -INFINITY) ? hyg_exp(tmp[n] - lz) : 0.0;
-      }
       /* updatePsi (:152-197) for every pending time */
       for (int s = 0; s < npend; ++s) {
         double* ps = pend[s].psi;
@@ -333,6 +353,8 @@ int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t see
       }
     }
     npend = keep;
+    oracle_sg_pending_sum += npend;
+    if (npend > oracle_sg_pending_max) oracle_sg_pending_max = npend;
   }
   rc = HYG_OK;
 done:

@@ -1,0 +1,164 @@
+"""Single-group throughput (BASELINE.json configs[1], "C2"): whole-genome
+synthetic, 28M CpG over 22 chromosomes, 4 samples, K = 6, N_max = 250,
+epsilon = 0.01, 1 seed on 1 GPU. One chain per chromosome, as the reference
+runs one R process per (sample group, chromosome); one "step" = emission table
++ SMC / optimal resampling / online marginal smoothing of every chain, counts
+resident in HBM. Prints one JSON line in bench.py's format (units = CpG sites).
+
+    python tools/bench_sg.py [--sites N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0
+
+
+def bytes_per_site(S: int, K: int) -> int:
+    """Unavoidable HBM bytes per site: uint16 counts (2 x S x 2 B) read by the
+    emission kernel, the f64 emission row written and read back (2 x 8K), the
+    f64 regime probabilities written (8K)."""
+    return 4 * S + 16 * K + 8 * K
+
+
+def cpu_baseline(meth, tot, chains, params, seconds, threads):
+    from oracle import sg_binding as sb
+
+    p = sb.SgParams.from_buffer_copy(bytes(params))
+    s0 = chains[0][0]
+    n_cal = 2000
+    t0 = time.perf_counter()
+    sb.chain(p, sb.emission(p, meth[s0:s0 + n_cal], tot[s0:s0 + n_cal]), 0, 1)
+    per_site = (time.perf_counter() - t0) / n_cal
+    n = int(max(2000, min(400000, seconds / per_site)))
+    res = [0] * threads
+
+    def work(i):
+        b = chains[i % len(chains)][0]
+        sl = slice(b, b + n)
+        out = sb.chain(p, sb.emission(p, meth[sl], tot[sl]), i, 7 + i)
+        assert out["status"] == 0
+        res[i] = n
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    return {"value": sum(res) / dt, "unit": "CpG-sites/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads x {n}-site prefixes of the chromosome chains, each one "
+                      f"oracle/sg_oracle.c emission + SMC + online smoothing; {sum(res)} sites in {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sites", type=int, default=28_000_000)
+    ap.add_argument("--samples", type=int, default=4)
+    ap.add_argument("--K", type=int, default=6)
+    ap.add_argument("--coverage", type=float, default=30.0)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=0)
+    ap.add_argument("--psi-capacity", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    from hygeia_amd import _lib, synthetic
+
+    dev = torch.device("cuda", 0)
+    L = _lib.load()
+    K, S = args.K, args.samples
+    d = synthetic.simulate_device(args.sites, S, 1, K=K, coverage=args.coverage, device=dev)
+    meth, tot = d["meth_control"], d["tot_control"]
+    del d["meth_case"], d["tot_case"]
+    sizes = synthetic.chromosome_sizes(args.sites)
+    begins = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    chains = sorted([(int(b), int(n), i) for i, (b, n) in enumerate(zip(begins, sizes))], key=lambda c: -c[1])
+    arr = (_lib.SgChain * len(chains))()
+    for i, (b, n, ci) in enumerate(chains):
+        arr[i].site_begin, arr[i].n_sites, arr[i].seed, arr[i].chain_id, arr[i].out_begin = b, n, 1, ci, b
+    max_reads = int(tot.to(torch.int32).max().item() & 0xFFFF)
+    p = _lib.SgParams()
+    L.hyg_sg_params_default(C.byref(p))  # pipeline defaults: K = 6, u = 3, N_max = 250, epsilon = 0.01
+    if K != p.n_regimes:
+        raise SystemExit("the C2 workload is K = 6")
+    h = C.c_void_p()
+    _lib.check(L.hyg_sg_model_create(C.byref(p), max_reads, int(max(sizes)), C.byref(h)))
+    wsb = int(L.hyg_sg_workspace_bytes(h, len(chains), args.psi_capacity))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    E = torch.empty((args.sites, K), dtype=torch.float64, device=dev)
+    probs = torch.empty((args.sites, K), dtype=torch.float64, device=dev)
+    st = torch.zeros(len(chains), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    kms = np.zeros(2)
+
+    def step(timed):
+        ev[0].record(stream)
+        _lib.check(L.hyg_sg_emission(h, meth.data_ptr(), tot.data_ptr(), S, args.sites, E.data_ptr(), sp))
+        ev[1].record(stream)
+        _lib.check(L.hyg_sg_run_chains(h, arr, len(chains), E.data_ptr(), ws.data_ptr(), wsb, args.psi_capacity,
+                                       probs.data_ptr(), st.data_ptr(), sp))
+        ev[2].record(stream)
+        if timed:
+            ev[2].synchronize()
+            kms[0] += ev[0].elapsed_time(ev[1])
+            kms[1] += ev[1].elapsed_time(ev[2])
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    status = st.cpu().numpy()
+    if (status != 0).any():
+        raise RuntimeError(f"chains failed: {np.unique(status)}")
+    pr = probs.sum(dim=1)
+    if not bool(((pr - 1.0).abs() < 1e-9).all().item()):
+        raise RuntimeError("regime probabilities do not sum to one")
+    ms = dt * 1000.0 / args.steps
+    kavg = kms / args.steps
+    bps = bytes_per_site(S, K)
+    line = {
+        "metric": "CpG sites/sec through SMC + online smoothing (single group)", "value": args.sites / (ms / 1000.0),
+        "unit": "CpG-sites/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"C2 single_group {args.sites} CpG, 22 chromosome chains, {S} samples, K={K}, "
+                               f"N_max=250, epsilon=0.01, 1 seed, coverage {args.coverage}",
+                   "chains": len(chains), "longest_chain": int(max(sizes)), "parallelism": "chains on 1 GPU"},
+        "roofline": {"bound": "hbm", "kernel": "sg_chain_kernel",
+                     "achieved": bps * args.sites / (kavg[1] / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": bps * args.sites / (kavg[1] / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                     "traffic": None, "bytes_per_unit": bps,
+                     "kernel_ms": {"sg_emission_kernel": float(kavg[0]), "sg_chain_kernel": float(kavg[1])},
+                     "us_per_step_longest_chain": float(kavg[1] * 1000.0 / max(sizes))},
+    }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(meth.cpu().numpy().view(np.uint16), tot.cpu().numpy().view(np.uint16),
+                                            chains, p, args.cpu_seconds, args.cpu_threads)
+    L.hyg_sg_model_destroy(h)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
