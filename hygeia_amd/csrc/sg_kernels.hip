@@ -96,9 +96,13 @@ struct SgLay {
 
 __host__ __device__ inline size_t sg_align(size_t x) { return (x + 15) / 16 * 16; }
 
+// NB = threads of the workgroup (particles live on threads < 256, the other
+// waves join the block reductions, sorts (on dummy keys) and the smoothing tasks)
+__host__ __device__ inline int sg_block_threads(int K) { return K <= 8 ? 512 : 256; }
+
 __host__ __device__ inline SgLay sg_layout(int K, int cap) {
   SgLay l{};
-  const int NT = kSgThreads, NW = NT / 64;
+  const int NT = kSgThreads, NB = sg_block_threads(K), NW = NB / 64;
   size_t o = 0;
   l.st = o; o = sg_align(o + 4 * 2 * NT);
   l.lw = o; o = sg_align(o + 8 * 2 * NT);
@@ -109,12 +113,12 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap) {
   l.lwres = o; o = sg_align(o + 8 * NT);
   l.logq = o; o = sg_align(o + 8 * NT);
   l.sidx = o; o = sg_align(o + 4 * NT);
-  l.cum = o; o = sg_align(o + 16 * (NT + 1));
-  l.xk = o; o = sg_align(o + 8 * 2 * NT);
-  l.xi = o; o = sg_align(o + 4 * 2 * NT);
+  l.cum = o; o = sg_align(o + 16 * (NB + 1));
+  l.xk = o; o = sg_align(o + 8 * 2 * NB);
+  l.xi = o; o = sg_align(o + 4 * 2 * NB);
   l.BK = o; o = sg_align(o + 8 * (size_t)K * NT);
   l.logP = o; o = sg_align(o + 8 * (size_t)K * K);
-  l.red = o; o = sg_align(o + 24 * (size_t)NW * K + 64);
+  l.red = o; o = sg_align(o + 24 * (size_t)NW * K + 16 * NW + 64);
   l.lsev = o; o = sg_align(o + 8 * 2 * (size_t)K);
   l.scr = o; o = sg_align(o + 8 * (size_t)NW * NT);
   l.meanb = o; o = sg_align(o + 8 * (size_t)kSgChunk * K);
@@ -123,7 +127,7 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap) {
   l.logQ = o; o = sg_align(o + 8 * (NT + 1));
   l.sh = o; o = sg_align(o + sizeof(SgShared));
   const size_t slot = 8 * (size_t)K * NT;
-  const size_t budget = 160 * 1024;
+  const size_t budget = 160 * 1024 - 2048;  // headroom below the 160 KiB of a CU (launches at 163808 B fail)
   int nl = o < budget ? (int)((budget - o) / slot) : 0;
   if (nl > 32) nl = 32;
   if (nl > cap) nl = cap;
@@ -190,8 +194,9 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 // oracle sort_desc); afterwards thread q holds the element of sorted position
 // q. Distances < 64 exchange through lane shuffles, 64 and 128 through LDS
 // (xk / xi, two buffers so consecutive cross-wave steps need one barrier each).
+template <int NB>
 __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk, int* xi) {
-  constexpr int NT = kSgThreads;
+  constexpr int NT = kSgThreads;  // the keys sorted: threads [0, 256) (threads >= 256 sort their own dummies)
   const int tid = threadIdx.x;
   int buf = 0;
 #pragma unroll
@@ -201,11 +206,11 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
       uint64_t pk;
       int pi;
       if (j >= 64) {
-        xk[buf * NT + tid] = key;
-        xi[buf * NT + tid] = idx;
+        xk[buf * NB + tid] = key;
+        xi[buf * NB + tid] = idx;
         lds_barrier();
-        pk = xk[buf * NT + (tid ^ j)];
-        pi = xi[buf * NT + (tid ^ j)];
+        pk = xk[buf * NB + (tid ^ j)];
+        pi = xi[buf * NB + (tid ^ j)];
         buf ^= 1;
       } else {
         pk = shfl_xor64(key, j);
@@ -232,12 +237,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 // and backward kernels, and the smoothing split into (pending time, regime)
 // tasks over all waves with the psi rows resident in LDS (up to 32 slots,
 // the rest in the chain's workspace region).
-template <int KT>
-__global__ void __launch_bounds__(kSgThreads)
+template <int KT, int NB>
+__global__ void __launch_bounds__(NB)
 sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const double* __restrict__ E,
                 uint8_t* __restrict__ ws, int cap, double* __restrict__ probs, int32_t* __restrict__ status_out,
                 SgLay lay, unsigned long long* __restrict__ dbg) {
-  constexpr int NT = kSgThreads, NW = NT / 64, K = KT;
+  constexpr int NT = kSgThreads, NW = NB / 64, K = KT;  // NT: particle slots, NB: threads
   const hyg_sg_consts& c = *md.consts;
   const int Nmax = c.Nmax, u = c.u, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   const double eps = c.epsilon;
@@ -279,9 +284,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
     return slot < nl ? psil + ((size_t)slot * K + r) * NT : psig + ((size_t)(slot - nl) * K + r) * NT;
   };
 
-  for (int i = tid; i < cap; i += NT) freel[i] = cap - 1 - i;
-  for (int i = tid; i < K * K; i += NT) logP[i] = c.logP[i];
-  for (int i = tid; i <= NT; i += NT) logm[i] = hyg_log((double)i);  // log(M - k) of the K loop
+  for (int i = tid; i < cap; i += NB) freel[i] = cap - 1 - i;
+  for (int i = tid; i < K * K; i += NB) logP[i] = c.logP[i];
+  for (int i = tid; i <= NT; i += NB) logm[i] = hyg_log((double)i);  // log(M - k) of the K loop
   // phase timers: 0 copy, 1 sort, 2 K loop, 3 residual / keep-top, 4 weights,
   // 5 normalise, 6 smoothing, 7 compaction; counters 8 optimal steps, 9
   // keep-top steps, 10 K-loop iterations, 11 pending entries, 15 = last stamp
@@ -309,13 +314,13 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   if (tid < K) sg_trans_parts(md, u, my_st, my_base, my_cont);
   double mx0;
   int fin;
-  block_max_cnt<NT>(my_lw, (tid < K && hyg_isfinite(my_lw)) ? 1 : 0, red, &mx0, &fin);
+  block_max_cnt<NB>(my_lw, (tid < K && hyg_isfinite(my_lw)) ? 1 : 0, red, &mx0, &fin);
   if (!(mx0 > HYG_NINF)) {
     if (tid == 0) status_out[blockIdx.x] = HYG_ENUMERIC;
     return;
   }
   double logZ =
-      mx0 + hyg_log(hyg_u128_to_f64(block_sum128<NT>(hyg_fix100(hyg_exp(my_lw - mx0)), red), 100));
+      mx0 + hyg_log(hyg_u128_to_f64(block_sum128<NB>(hyg_fix100(hyg_exp(my_lw - mx0)), red), 100));
   double my_w = (tid < K) ? hyg_exp(my_lw - logZ) : 0.0;
   if (tid < K) {
     st_[tid] = my_st;
@@ -350,35 +355,50 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       // ---- resampleCp (:406-450)
       if (N < Np + K) {
         bool keep_top = true;
+        // order by log-weight (the keep-top fallback's order, Smc.h:432-441)
+        uint64_t lkey = (tid < Np) ? sg_okey(plw) : 0;
+        int lidx = tid;
+        sg_bitonic<NB>(lkey, lidx, xk, xi);
+        const double* wP = w_ + pb * NT;
         if (fin > M) {
-          // optimalFiniteState (resample.h:289-409) on the sorted self-normalised weights
-          uint64_t key = (tid < Np) ? sg_okey(pw) : 0;
-          int idx = tid;
-          sg_bitonic(key, idx, xk, xi);
+          // optimalFiniteState (resample.h:289-409) on the weights sorted
+          // descending. The K loop needs only the sorted values: when w is
+          // non-increasing along the log-weight order, that order carries
+          // them; otherwise (or for the index order the optimal branch
+          // assigns) the exact sort by w, ties by index, is run.
+          double q = (tid < Np) ? wP[lidx] : 0.0;
+          if (tid < NT) logq[tid] = q;
+          lds_barrier();
+          const bool mono = !__syncthreads_or(tid + 1 < Np && logq[tid + 1] > q);
+          int idx = lidx;
+          if (!mono) {
+            uint64_t key = (tid < Np) ? sg_okey(pw) : 0;
+            idx = tid;
+            sg_bitonic<NB>(key, idx, xk, xi);
+            q = (tid < Np) ? sg_okey_value(key) : 0.0;
+          }
           double lq = HYG_NINF;
           hyg_u128 mq = hyg_u128_zero();
           if (tid < Np) {
-            const double q = sg_okey_value(key);
             lq = hyg_log(q);
             mq = hyg_fix100(q);
           }
-          logq[tid] = lq;
-          sidx[tid] = idx;
+          if (tid < NT) {
+            logq[tid] = lq;
+            sidx[tid] = idx;
+          }
           // reverse cumulative sums Q(k) = total - exclusive prefix (exact)
-          block_scan128<NT>(mq, cum, red);
+          block_scan128<NB>(mq, cum, red);
           lds_barrier();
           {
-            const hyg_u128 tot = cum[NT], ex = cum[tid];
+            const hyg_u128 tot = cum[NB], ex = cum[tid];
             hyg_u128 suf;
             suf.lo = tot.lo - ex.lo;
             suf.hi = tot.hi - ex.hi - (tot.lo < ex.lo ? 1u : 0u);
             lds_barrier();
             cum[tid] = suf;
-            logQ[tid] = hyg_log(hyg_u128_to_f64(suf, 100));
-            if (tid == 0) {
-              cum[NT] = hyg_u128_zero();
-              logQ[NT] = HYG_NINF;
-            }
+            if (tid <= NT) logQ[tid] = hyg_log(hyg_u128_to_f64(suf, 100));
+            if (NB == NT && tid == 0) logQ[NT] = HYG_NINF;
           }
           lds_barrier();
           SG_PH(1);
@@ -415,6 +435,12 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           const double logC = sh.logC;
           if (hyg_isfinite(logC)) {
             keep_top = false;
+            if (mono) {  // the exact index order among equal weights
+              uint64_t key = (tid < Np) ? sg_okey(pw) : 0;
+              idx = tid;
+              sg_bitonic<NB>(key, idx, xk, xi);
+              if (tid < NT) sidx[tid] = idx;
+            }
             const int Kk = sh.Kk, L = M - Kk;
             if (tid < Kk) {
               anc[tid] = idx;
@@ -424,9 +450,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
               // residual systematic draw (:372-377, systematicBase :85-117):
               // T_j = (j + u) / L <= Q_i as exact C_i >= ceil(T_j R)
               const bool inres = tid >= Kk && tid < Np;
-              const double rmax = block_max<NT>(inres ? lq : HYG_NINF, red);
+              const double rmax = block_max<NB>(inres ? lq : HYG_NINF, red);
               const hyg_u128 m2 = inres ? hyg_fix100(hyg_exp(lq - rmax)) : hyg_u128_zero();
-              block_scan128<NT>(m2, cum, red);
+              block_scan128<NB>(m2, cum, red);
               const hyg_u128 incl = hyg_u128_add(cum[tid], m2);
               lds_barrier();
               cum[tid] = incl;
@@ -449,15 +475,10 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
             }
           }
         }
-        if (keep_top) {
+        if (keep_top && tid < M) {
           // keep the M largest log-weights (Smc.h:432-441, resample.h:379-384)
-          uint64_t key = (tid < Np) ? sg_okey(plw) : 0;
-          int idx = tid;
-          sg_bitonic(key, idx, xk, xi);
-          if (tid < M) {
-            anc[tid] = idx;
-            lwres[tid] = lwP[idx];
-          }
+          anc[tid] = lidx;
+          lwres[tid] = lwP[lidx];
         }
         SG_CNT(8, keep_top ? 0 : 1);
         SG_CNT(9, keep_top ? 1 : 0);
@@ -552,12 +573,12 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       SG_PH(4);
       // ---- selfNormaliseWeights (:576-579)
       double mx;
-      block_max_cnt<NT>(nlw, (tid < N && hyg_isfinite(nlw)) ? 1 : 0, red, &mx, &fin);
+      block_max_cnt<NB>(nlw, (tid < N && hyg_isfinite(nlw)) ? 1 : 0, red, &mx, &fin);
       if (!(mx > HYG_NINF)) {
         status = HYG_ENUMERIC;
         break;
       }
-      logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NT>(hyg_fix100(hyg_exp(nlw - mx)), red), 100));
+      logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NB>(hyg_fix100(hyg_exp(nlw - mx)), red), 100));
       my_lw = nlw;
       my_st = nst;
       my_w = (tid < N) ? hyg_exp(nlw - logZ) : 0.0;
@@ -704,14 +725,14 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       int32_t* slotB = lists + (size_t)(cur ^ 1) * 2 * cap;
       int32_t* timeB = slotB + cap;
       int nk = 0, nf = sh.nfree;
-      for (int b = 0; b < ntot; b += NT) {
+      for (int b = 0; b < ntot; b += NB) {
         const int e = b + tid;
         const bool in = e < ntot;
         const int kp = in ? keepf[e] : 0;
         const int sl = in ? slotA[e] : 0;
         const int v = in ? (kp ? 1 : (sl >= nl ? 0x10000 : 0)) : 0;
         int tot;
-        const int ex = block_excl_int<NT>(v, red, &tot);
+        const int ex = block_excl_int<NB>(v, red, &tot);
         if (in) {
           if (kp) {
             const int p = nk + (ex & 0xffff);
@@ -748,14 +769,14 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
 }
 
 // ------------------------------------------------------------- launches
-template <int KT>
+template <int KT, int NB>
 static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, int n_chains, const double* E,
                             uint8_t* ws, int cap, double* probs, int32_t* status, const SgLay& lay,
                             unsigned long long* dbg, hipStream_t s, hipError_t* err) {
-  *err = hipFuncSetAttribute((const void*)sg_chain_kernel<KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  *err = hipFuncSetAttribute((const void*)sg_chain_kernel<KT, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lay.total);
   if (*err != hipSuccess) return;
-  hipLaunchKernelGGL(sg_chain_kernel<KT>, dim3(n_chains), dim3(kSgThreads), lay.total, s, md, chains_dev, E, ws,
+  hipLaunchKernelGGL((sg_chain_kernel<KT, NB>), dim3(n_chains), dim3(NB), lay.total, s, md, chains_dev, E, ws,
                      cap, probs, status, lay, dbg);
   *err = hipGetLastError();
 }
@@ -785,7 +806,7 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
   hipError_t err = hipErrorInvalidValue;
   switch (c.K) {
 #define SG_CASE(k) \
-  case k: launch_chain_kt<k>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, dbg, s, &err); break;
+  case k: launch_chain_kt<k, (k <= 8 ? 512 : 256)>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, dbg, s, &err); break;
     SG_CASE(2) SG_CASE(3) SG_CASE(4) SG_CASE(5) SG_CASE(6) SG_CASE(7) SG_CASE(8) SG_CASE(9)
     SG_CASE(10) SG_CASE(11) SG_CASE(12) SG_CASE(13) SG_CASE(14) SG_CASE(15) SG_CASE(16)
 #undef SG_CASE

@@ -134,6 +134,7 @@ typedef struct {
 /* diagnostics: sum / max over steps of the number of pending smoothing times */
 int64_t oracle_sg_pending_sum = 0;
 int32_t oracle_sg_pending_max = 0;
+int64_t oracle_sg_optimal_steps = 0; /* capped steps resampled by the optimal scheme (finite log c) */
 
 /* One chain over T sites: E [T][K] emission table. Writes probs [T][K]
  * (the smoothed regime probabilities). Returns HYG_OK / HYG_ENUMERIC / HYG_ENOMEM. */
@@ -228,6 +229,7 @@ int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t see
           }
           if (hyg_isfinite(logC)) {
             keep_top = 0;
+            ++oracle_sg_optimal_steps;
             const int Kk = kNew, L = M - Kk;
             for (int q = 0; q < Kk; ++q) {
               anc[q] = idx[q];
