@@ -598,7 +598,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
     int32_t* timeA = slotA + cap;
     if (tid == 0) {
       int slot = -1;
-      if (sh.lmask) {
+      if (nold >= cap) {
+        slot = -1;  // the pending list holds cap entries
+      } else if (sh.lmask) {
         const int b = __builtin_ctz(sh.lmask);
         sh.lmask &= ~(1u << b);
         slot = b;
