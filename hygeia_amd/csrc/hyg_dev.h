@@ -54,6 +54,44 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
   return ((uint64_t)hi << 32) | lo;
 }
+// Value of lane (lane ^ LM) for LM = 1..32: quad perms, row shifts, row_ror:8
+// and the gfx950 permlane16/32 swaps (no LDS round trip).
+template <int LM>
+__device__ __forceinline__ uint32_t xshfl32(uint32_t v) {
+  static_assert(LM == 1 || LM == 2 || LM == 4 || LM == 8 || LM == 16 || LM == 32, "lane xor mask");
+  if constexpr (LM == 1) {
+    return dpp32<kDppQuad1032>(v);
+  } else if constexpr (LM == 2) {
+    return dpp32<kDppQuad2301>(v);
+  } else if constexpr (LM == 4) {
+    const uint32_t up = dpp32<0x104>(v), dn = dpp32<0x114>(v);  // row_shl:4 / row_shr:4
+    return (threadIdx.x & 4) ? dn : up;
+  } else if constexpr (LM == 8) {
+    return dpp32<0x128>(v);  // row_ror:8
+  } else if constexpr (LM == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? r[0] : r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? r[0] : r[1];
+  }
+}
+template <int LM>
+__device__ __forceinline__ uint64_t xshfl64(uint64_t v) {
+  return ((uint64_t)xshfl32<LM>((uint32_t)(v >> 32)) << 32) | xshfl32<LM>((uint32_t)v);
+}
+// LDS hand-off between the lanes of one wave (no workgroup barrier)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+// number of set bits of `mask` below this lane
+__device__ __forceinline__ int lanes_below(uint64_t mask) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
 __device__ __forceinline__ double d_of(uint64_t u) { return __builtin_bit_cast(double, u); }
 __device__ __forceinline__ uint64_t u_of(double d) { return __builtin_bit_cast(uint64_t, d); }
 
@@ -115,6 +153,11 @@ __device__ __forceinline__ hyg_u192 wave_incl192(hyg_u192 v) {
   v = hyg_u192_add(v, dpp192<kDppRowBcast15, 0xa>(v));
   v = hyg_u192_add(v, dpp192<kDppRowBcast31, 0xc>(v));
   return v;
+}
+__device__ __forceinline__ hyg_u192 rdlane192(hyg_u192 v, int l) {
+  hyg_u192 r;
+  r.w0 = rdlane64(v.w0, l); r.w1 = rdlane64(v.w1, l); r.w2 = rdlane64(v.w2, l);
+  return r;
 }
 template <int CTRL, int RM>
 __device__ __forceinline__ hyg_u128 dpp128(hyg_u128 v) {

@@ -225,11 +225,6 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
     }
   }
 }
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-}
 
 // One workgroup per chain, thread n = particle n (N_max <= 256). Per step the
 // critical path is a few dozen barriers: sorts in registers, the K / log c

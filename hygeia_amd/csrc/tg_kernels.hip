@@ -173,17 +173,19 @@ __device__ __forceinline__ Hz4 child_hz(const ConstLds& cl, int K, uint64_t a, i
                                         const ModelDev& md) {
   Hz4 h;
   const uint64_t x = tg_xi(K, a, s);
-  double2 hc, hk;
-  if (s == 0) { hc = p.c1; hk = p.k1; }
-  else if (s < K) { hc = cl.hz1[0][hyg_st_rc(x)]; hk = p.k1; }
-  else if (s < 2 * K - 1) { hc = p.c1; hk = cl.hz1[1][hyg_st_rk(x)]; }
-  else if (s == 2 * K - 1) {
-    if (hyg_st_m(a) == 0) { hc = p.c1; hk = p.kc; }
-    // m = 1: the merge slot's child (1, 0, r, 0, r) has weight -inf, is never
-    // resampled and never becomes an ancestor; its hazards are never used
-    else { hc = cl.hz1[0][hyg_st_rc(x)]; hk = cl.hz1[1][hyg_st_rk(x)]; }
-  } else { hc = cl.hz1[0][hyg_st_rc(x)]; hk = cl.hz1[1][hyg_st_rk(x)]; }
-  h.lrc = hc.x; h.l1c = hc.y; h.lrk = hk.x; h.l1k = hk.y;
+  // s == 0: both durations continue; s < K: control changes; s < 2K-1: case
+  // changes; s == 2K-1 with m = 0: merge (case continues on the control row);
+  // m = 1 there: the merge slot's child (1, 0, r, 0, r) has weight -inf, is
+  // never resampled and never becomes an ancestor, so its hazards are unused.
+  // Value selects (a select of addresses would put p in scratch memory).
+  const double2 h1c = cl.hz1[0][hyg_st_rc(x)], h1k = cl.hz1[1][hyg_st_rk(x)];
+  const bool merge = (s == 2 * K - 1) && hyg_st_m(a) == 0;
+  const bool c_cont = s == 0 || (s >= K && s < 2 * K - 1) || merge;
+  const bool k_cont = s < K;
+  h.lrc = c_cont ? p.c1.x : h1c.x;
+  h.l1c = c_cont ? p.c1.y : h1c.y;
+  h.lrk = merge ? p.kc.x : (k_cont ? p.k1.x : h1k.x);
+  h.l1k = merge ? p.kc.y : (k_cont ? p.k1.y : h1k.y);
   return h;
 }
 
@@ -210,21 +212,27 @@ __device__ __forceinline__ uint64_t tg_xi_hz_sel(const ConstLds& cl, int K, floa
   // hazard rows: prefetched rows where the duration continues, d = 1 rows at a change
   const bool c_cont = tA || (!tB && tC) || (tD && m == 0);
   const bool k_cont = tA || (tB && !tA);
-  const double2 hc = c_cont ? p.c1 : cl.hz1[0][xrc];
-  const double2 hk = (tD && m == 0) ? p.kc : (k_cont ? p.k1 : cl.hz1[1][xrk]);
-  hout->lrc = hc.x; hout->l1c = hc.y; hout->lrk = hk.x; hout->l1k = hk.y;
+  // (value selects: a select of the address would put p in scratch memory)
+  const double2 h1c = cl.hz1[0][xrc], h1k = cl.hz1[1][xrk];
+  const bool kc = tD && m == 0;
+  hout->lrc = c_cont ? p.c1.x : h1c.x;
+  hout->l1c = c_cont ? p.c1.y : h1c.y;
+  hout->lrk = kc ? p.kc.x : (k_cont ? p.k1.x : h1k.x);
+  hout->l1k = kc ? p.kc.y : (k_cont ? p.k1.y : h1k.y);
   return hyg_st_pack(xm, xdc, xrc, xdk, xrk);
 }
 
 // ------------------------------------------------------------ LDS layout
+constexpr int kPh = 32;  // diagnostic phase timers (last entry: timestamp / step count)
+
 struct Shared {  // broadcast scalars of one workgroup
   double mx, logS;
   float c_new, log_c;
-  int cnt, n_sig, Kk, status, r_ph, ng;
+  int cnt, n_sig, Kk, status, r_ph, ng, fast;
   float Unext;  // systematic-resampling uniform of the next step, drawn during the gather
   unsigned sig_ctr;
   hyg_u192 R, preK;
-  unsigned long long ph[24];
+  unsigned long long ph[kPh];
 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -235,9 +243,11 @@ __host__ __device__ inline int next_pow2(int x) {
 }
 
 constexpr int kBuckets = 512;  // counting-sort buckets of the resampling sort (sqrt-spaced in -lw)
+constexpr int kNCut = 8;       // log-weight cutoffs of the top-set resampling path
 
 struct Lay {  // byte offsets into the dynamic LDS
-  size_t W, L, keys, bcnt, bpos, pre64, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, red, sh, total;
+  size_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, red, sh, total;
+  size_t bcnt_bytes;
   int npad, nkeys, nt;
 };
 
@@ -262,8 +272,11 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
     if (bb < sizeof(hyg_u192) * (size_t)M) bb = sizeof(hyg_u192) * (size_t)M;
     l.bcnt = o;
     l.bpos = o + sizeof(int) * kBuckets;
+    l.bcnt_bytes = bb;
     o = align_up(o + bb, 16);
     l.pre64 = o; o = align_up(o + sizeof(hyg_u192) * (M < 64 ? M : 64), 16);
+    // per-wave partials of the top-set resampling path (counts per cutoff, mass)
+    l.part = o; o = align_up(o + (sizeof(int) * kNCut + sizeof(hyg_u192)) * (NT / 64), 16);
   }
   // the ancestors of the current step (single buffer: rewritten behind a barrier)
   l.pst = o; o = align_up(o + sizeof(uint64_t) * M, 16);
@@ -538,8 +551,8 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
 #define SPH(k)                                                     \
   if (timed && tid == 0) {                                         \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-    ph[k] += now_ - ph[23];                                        \
-    ph[23] = now_;                                                 \
+    ph[k] += now_ - ph[kPh - 1];                                        \
+    ph[kPh - 1] = now_;                                                 \
   }
   // any monotone map works (the order inside a bucket is resolved exactly);
   // sqrt spacing puts narrow buckets where the weights crowd, near the top
@@ -778,6 +791,278 @@ __device__ void optimal_resample(const double* W, uint64_t* sorted, int N, doubl
 #undef SPH
 }
 
+// ------------------------------------------- resampling: the top-set path
+// OptimalFiniteState touches the order of the largest log-weights only: the
+// K / log c search reads the prefix masses of the first a < M sorted weights
+// and counts #{p : fl(c + x_p) > 0}, and the systematic targets land where
+// the cumulative residual mass crosses them (at C3 the deepest draw sits near
+// sorted rank 300 of ~900 significant weights). This path sorts exactly only
+// the top set A = {lw >= cut} for the most inclusive of kNCut cutoffs whose
+// set fits one block bitonic sort (<= 128 keys per wave), takes the total
+// mass of every significant weight from an order-free exact sum, and then
+// checks with exact quantities that each index decision falls inside A:
+//   - every K-loop probe the loop visits has its prefix and its count in A;
+//   - the last systematic target lies at or below the mass of A.
+// If a check fails the caller runs the full counting-sort path
+// (optimal_resample), so the parents are those of the full sort either way.
+enum { FAST_DONE = 0, FAST_FALLBACK = 1, FAST_FALLBACK_REGEN = 2 };
+#define TPH(k)                                                     \
+  if (timed && threadIdx.x == 0) {                                 \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    ph[k] += now_ - ph[kPh - 1];                                   \
+    ph[kPh - 1] = now_;                                            \
+  }
+
+// log-weight cutoffs below the top weight (nats); the last is sig_thresh
+__device__ __forceinline__ float cut_below_top(int k) {
+  constexpr float x[kNCut - 1] = {8.0f, 12.0f, 16.0f, 20.0f, 25.0f, 32.0f, 45.0f};
+  return x[k];
+}
+
+// One compare-exchange stage (k, j) of a bitonic sort of 64*NW*R keys held
+// R per lane, key index i = wave*64R + lane*R + r (ascending result).
+// j < R: inside the lane; j < 64R: lane xor shuffles; else: LDS + barrier.
+template <int NT, int R, int KK, int J>
+__device__ __forceinline__ void bitonic_stage(uint64_t (&e)[R], uint64_t* buf, int& ib) {
+  constexpr int n = 64 * (NT / 64) * R;
+  const int base = (int)(threadIdx.x >> 6) * 64 * R + lane_id() * R;
+  if constexpr (J < R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int pr = r ^ J;
+      if (pr > r) {
+        const bool up = ((base + r) & KK) == 0;
+        const uint64_t a = e[r], b = e[pr];
+        const bool sw = up ? (a > b) : (a < b);
+        e[r] = sw ? b : a;
+        e[pr] = sw ? a : b;
+      }
+    }
+  } else if constexpr (J < 64 * R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t o = xshfl64<J / R>(e[r]);
+      const int i = base + r;
+      const bool keep_min = ((i & J) == 0) == ((i & KK) == 0);
+      const bool lt = o < e[r];
+      e[r] = (keep_min == lt) ? o : e[r];
+    }
+  } else {
+    uint64_t* b = buf + (ib & 1) * n;  // alternate buffers: one barrier per stage
+    ++ib;
+#pragma unroll
+    for (int r = 0; r < R; ++r) b[base + r] = e[r];
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = base + r;
+      const uint64_t o = b[i ^ J];
+      const bool keep_min = ((i & J) == 0) == ((i & KK) == 0);
+      const bool lt = o < e[r];
+      e[r] = (keep_min == lt) ? o : e[r];
+    }
+  }
+}
+template <int NT, int R, int KK, int J>
+struct Bitonic {
+  __device__ static __forceinline__ void run(uint64_t (&e)[R], uint64_t* buf, int& ib) {
+    bitonic_stage<NT, R, KK, J>(e, buf, ib);
+    if constexpr (J > 1) Bitonic<NT, R, KK, J / 2>::run(e, buf, ib);
+    else if constexpr (KK < 64 * (NT / 64) * R) Bitonic<NT, R, 2 * KK, KK>::run(e, buf, ib);
+  }
+};
+
+// Sort A (nA keys in srt[]), exact prefix masses, the K / log c loop and the
+// systematic draws. scr: the W + key areas (W is overwritten).
+template <int NT, int R>
+__device__ int top_set_finish(uint64_t* srt, int nA, int n_sig, int N, int M, int cnt_fin, const hyg_u192& total,
+                              unsigned char* scr, int* parents, Shared& sh, const ConstLds& cl, unsigned char* red,
+                              float Usys, unsigned long long* ph, bool timed) {
+  const int lane = lane_id();
+  const int base = (int)(threadIdx.x >> 6) * 64 * R + lane * R;
+  uint64_t e[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) e[r] = (base + r < nA) ? srt[base + r] : ~0ull;
+  int ib = 0;
+  Bitonic<NT, R, 2, 1>::run(e, (uint64_t*)scr, ib);
+  TPH(27);
+  // (every wave loaded its keys before the first cross-wave barrier)
+#pragma unroll
+  for (int r = 0; r < R; ++r) srt[base + r] = e[r];
+  hyg_u192 f[R];
+  hyg_u192 loc = hyg_u192_zero();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float m = hyg_expf(key_value(e[r]));
+    f[r] = hyg_fix149f((base + r < nA) ? m : 0.0f);
+    loc = hyg_u192_add(loc, f[r]);
+  }
+  hyg_u192 massA;
+  const hyg_u192 ex = block_excl192<NT>(loc, red, &massA);  // its barriers end every sort-buffer read
+  hyg_u192* pre = (hyg_u192*)scr;                           // inclusive prefix of sorted position p
+  hyg_u192 run = ex;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    run = hyg_u192_add(run, f[r]);
+    if (base + r < nA) pre[base + r] = run;
+  }
+  lds_barrier();
+  TPH(28);
+  if (wave_id() == 0) {
+    // lane a: c(a) and the count P(c(a)) (loop-variable semantics of :12-31)
+    const int a = lane;
+    int Pa = 0, flag = 0;
+    float ca = 0.0f;
+    hyg_u192 rva = hyg_u192_zero();
+    if (a < M && a < N) {
+      if (a < n_sig) {
+        if (a <= nA) rva = hyg_u192_sub(total, a == 0 ? hyg_u192_zero() : pre[a - 1]);
+        else flag = 1;  // prefix outside A
+      }
+      const double rvd = hyg_u192_to_f64(rva);
+      const float l2 = (rvd == 0.0) ? HYG_NINFF : (float)hyg_log(rvd);
+      ca = cl.logMa[a] - l2;
+      if (hyg_isfinitef(ca)) {
+        int lo = 0, hi = nA;  // first p with the predicate false
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if ((float)(ca + key_value(srt[mid])) > 0.0f) lo = mid + 1; else hi = mid;
+        }
+        Pa = lo;
+        if (lo == nA && nA < n_sig) flag = 1;  // the count may continue below A
+      } else if (ca > 0.0f) {
+        Pa = cnt_fin;
+      }
+    }
+    int aa = 0, bb = -1, ovf = 0;
+    while (aa != bb && aa < N && aa < M) {
+      const int nxt = __builtin_amdgcn_readlane(Pa, aa);
+      ovf |= __builtin_amdgcn_readlane(flag, aa);
+      bb = aa;
+      aa = nxt > aa ? nxt : aa;
+    }
+    const float lc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), bb));
+    const hyg_u192 Rr = rdlane192(rva, bb);
+    int status = FAST_DONE;
+    if (ovf) {
+      status = FAST_FALLBACK_REGEN;
+    } else if (bb < N && hyg_isfinitef(lc)) {
+      // systematic residual (:32-40, :56-69): target j lands on the first
+      // sorted position p >= K with C(p) >= preK + ceil(T_j R)
+      const int L = M - bb;
+      const hyg_u192 preK = hyg_u192_sub(total, Rr);
+      hyg_u192 tau = hyg_u192_zero();
+      if (lane < L) tau = hyg_u192_add(preK, hyg_ceil_mul_f32(((float)lane + Usys) / (float)L, Rr));
+      const hyg_u192 tlast = rdlane192(tau, L > 0 ? L - 1 : 0);
+      if (L > 0 && nA < n_sig && !hyg_u192_ge(massA, tlast)) {
+        status = FAST_FALLBACK_REGEN;
+      } else {
+        if (lane < bb) parents[lane] = key_index(srt[lane]);
+        if (lane < L) {
+          int lo = bb, hi = nA - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (hyg_u192_ge(pre[mid], tau)) hi = mid; else lo = mid + 1;
+          }
+          parents[bb + lane] = key_index(srt[lo]);
+        }
+      }
+    }
+    if (lane == 0) {
+      sh.Kk = bb;
+      sh.log_c = lc;
+      sh.fast = status;
+    }
+  }
+  lds_barrier();
+  TPH(29);
+  return sh.fast;
+}
+
+// Top-set path of OptimalFiniteState; returns FAST_DONE (parents / Kk /
+// log_c written; log_c infinite -> the caller's unbiased fallback),
+// FAST_FALLBACK (W intact) or FAST_FALLBACK_REGEN (W overwritten).
+template <int NT>
+__device__ int top_set_resample(const double* W, int N, double mx, double logS, float thr, const int* lst, int lb,
+                                int cw,
+                                unsigned char* scr, size_t scr_bytes, uint64_t* srt, size_t srt_bytes, int* part_cnt,
+                                hyg_u192* part_tot, int* parents, Shared& sh, const ConstLds& cl,
+                                unsigned char* red, int M, int cnt_fin, float Usys, unsigned long long* ph,
+                                bool timed) {
+  constexpr int NW = NT / 64;
+  const int wv = wave_id(), lane = lane_id();
+  const float lwtop = (float)((mx - mx) - logS);  // the largest log-weight
+  float cut[kNCut];
+#pragma unroll
+  for (int k = 0; k < kNCut - 1; ++k) {
+    const float v = lwtop - cut_below_top(k);
+    cut[k] = v > thr ? v : thr;
+  }
+  cut[kNCut - 1] = thr;
+  // ---- 1. per wave, over its list of candidates with W - mx >= sig_thresh:
+  //         exact mass sum of the significant ones and counts per cutoff
+  hyg_u192 ms = hyg_u192_zero();
+  int cc[kNCut];
+#pragma unroll
+  for (int k = 0; k < kNCut; ++k) cc[k] = 0;
+  for (int i = 0; i < cw; i += 64) {
+    const bool v = i + lane < cw;
+    const int n = lst[lb + (v ? i + lane : cw - 1)];
+    const float lw = (float)((W[n] - mx) - logS);
+    const bool sig = v && lw >= thr;
+    const float m = hyg_expf(lw);
+    ms = hyg_u192_add(ms, hyg_fix149f(sig ? m : 0.0f));
+#pragma unroll
+    for (int k = 0; k < kNCut; ++k) cc[k] += (int)__builtin_popcountll(wave_ballot(sig && lw >= cut[k]));
+  }
+  const hyg_u192 wsum = rdlane192(wave_incl192(ms), 63);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < kNCut; ++k) part_cnt[wv * kNCut + k] = cc[k];
+    part_tot[wv] = wsum;
+  }
+  lds_barrier();
+  TPH(25);
+  // ---- 2. the most inclusive cutoff whose set fits the sort; gather A
+  int ks = -1, nA = 0;
+  int n_sig = 0;
+#pragma unroll
+  for (int k = 0; k < kNCut; ++k) {
+    int c = 0;
+    for (int w = 0; w < NW; ++w) c += part_cnt[w * kNCut + k];
+    const int np = (c <= 64 * NW) ? 64 * NW : 128 * NW;
+    if (c <= 128 * NW && (size_t)np * sizeof(hyg_u192) <= scr_bytes && (size_t)np * 8 <= srt_bytes) {
+      ks = k;
+      nA = c;
+    }
+    n_sig = c;
+  }
+  if (threadIdx.x == 0) sh.n_sig = n_sig;
+  if (ks < 0) return FAST_FALLBACK;  // uniform
+  hyg_u192 total = hyg_u192_zero();
+  int off = 0;
+  for (int w = 0; w < NW; ++w) {
+    total = hyg_u192_add(total, part_tot[w]);
+    if (w < wv) off += part_cnt[w * kNCut + ks];
+  }
+  const float cs = cut[ks];
+  for (int i = 0; i < cw; i += 64) {
+    const bool v = i + lane < cw;
+    const int n = lst[lb + (v ? i + lane : cw - 1)];
+    const float lw = (float)((W[n] - mx) - logS);
+    const bool sel = v && lw >= cs;
+    const uint64_t bal = wave_ballot(sel);
+    if (sel) srt[off + lanes_below(bal)] = sort_key(lw, n);
+    off += (int)__builtin_popcountll(bal);
+  }
+  lds_barrier();
+  TPH(26);
+  if (nA <= 64 * NW)
+    return top_set_finish<NT, 1>(srt, nA, n_sig, N, M, cnt_fin, total, scr, parents, sh, cl, red, Usys, ph, timed);
+  return top_set_finish<NT, 2>(srt, nA, n_sig, N, M, cnt_fin, total, scr, parents, sh, cl, red, Usys, ph, timed);
+}
+#undef TPH
+
 // --------------------------------------------------------------- kernels
 __global__ void __launch_bounds__(256)
 tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg, const double* __restrict__ cst,
@@ -813,8 +1098,9 @@ tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
   }
 }
 
+// 3 workgroups per CU at NT = 256 (<= 168 VGPRs): all C3 chains resident at once
 template <int NT>
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT, (NT <= 256 ? 3 : 1))
 tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                   uint8_t* __restrict__ ws, int32_t* status_out, double* __restrict__ logz_out,
                   double* __restrict__ finalw_out, Lay lay, unsigned long long* __restrict__ dbg) {
@@ -839,15 +1125,17 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
   int* parents = (int*)(smem + lay.parents);
   unsigned char* red = smem + lay.red;
   Shared& sh = *(Shared*)(smem + lay.sh);
+  int* part_cnt = (int*)(smem + lay.part);
+  hyg_u192* part_tot = (hyg_u192*)(smem + lay.part + sizeof(int) * kNCut * (NT / 64));
 
   // phase timers (diagnostic runs only: dbg != nullptr), kept in LDS
   unsigned long long* ph_acc = sh.ph;
-  if (tid < 24) ph_acc[tid] = 0;
+  if (tid < kPh) ph_acc[tid] = 0;
 #define PH(k)                                                      \
   if (dbg && tid == 0) {                                           \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-    ph_acc[k] += now_ - ph_acc[23];                                \
-    ph_acc[23] = now_;                                             \
+    ph_acc[k] += now_ - ph_acc[kPh - 1];                                \
+    ph_acc[kPh - 1] = now_;                                             \
   }
 
   uint8_t* rec0 = ws + ch.ws_offset;
@@ -876,7 +1164,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
   int cnt;
   block_max_cnt<NT>(mloc, cloc, red, &mx, &cnt);
 
-  if (dbg && tid == 0) ph_acc[23] = __builtin_amdgcn_s_memtime();
+  if (dbg && tid == 0) ph_acc[kPh - 1] = __builtin_amdgcn_s_memtime();
   for (int t = 1; t < T; ++t) {
     // emission rows one block ahead: issue at the block start, land in the ring later
     const bool eload = ((t % kEBlock) == 0) && (t + kEBlock < T);
@@ -887,13 +1175,35 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     }
     const float Ucur = sh.Unext;  // written during step t-1's gather, before two barriers
     // ---- log_softmax / reduce_logsumexp of the weights of step t-1
+    // ---- per wave, the list of candidates with W - mx >= sig_thresh (keys
+    //      area): every nonzero F=100 mass (x >= -70) and every significant
+    //      f32 log-weight is on it; candidates interleaved over the waves
+    int* lst = (int*)keys;
+    const int lst_base = wave_id() * (((N + NT - 1) / NT) * 64);
+    int lst_cnt = 0;
+    {
+      const double cutw = (double)c->sig_thresh;
+      for (int b = wave_id() * 64; b < N; b += NT) {
+        const int n = b + lane_id();
+        const bool keep = (n < N) && (W[n] - mx >= cutw);
+        const uint64_t bal = wave_ballot(keep);
+        if (keep) lst[lst_base + lst_cnt + lanes_below(bal)] = n;
+        lst_cnt += (int)__builtin_popcountll(bal);
+      }
+      wave_lds_sync();
+    }
     double logS;
     {
-      hyg_u128 sacc = hyg_u128_zero();
-      // branch-free body (fix100(exp(x)) is 0 for every x < -70, so the
-      // oracle's skip needs no test here), unrolled for ILP
-#pragma unroll 4
-      for (int n = tid; n < N; n += NT) sacc = hyg_u128_add(sacc, hyg_fix100(hyg_exp(W[n] - mx)));
+      // two independent chains per iteration; fix100(exp(x)) is 0 for x < -70
+      hyg_u128 s0 = hyg_u128_zero(), s1 = hyg_u128_zero();
+      int i = lane_id();
+      for (; i + 64 < lst_cnt; i += 128) {
+        const double x0 = W[lst[lst_base + i]] - mx, x1 = W[lst[lst_base + i + 64]] - mx;
+        s0 = hyg_u128_add(s0, hyg_fix100(hyg_exp(x0)));
+        s1 = hyg_u128_add(s1, hyg_fix100(hyg_exp(x1)));
+      }
+      if (i < lst_cnt) s0 = hyg_u128_add(s0, hyg_fix100(hyg_exp(W[lst[lst_base + i]] - mx)));
+      const hyg_u128 sacc = hyg_u128_add(s0, s1);
       PH(12);
       const hyg_u128 S = block_sum128<NT>(sacc, red);
       PH(11);
@@ -924,8 +1234,27 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     } else {
       // ---- OptimalFiniteState (resampling_functions.py:7-52)
       PH(2);
-      optimal_resample<NT>(W, (uint64_t*)W, N, mx, logS, c->sig_thresh, keys, bcnt, bpos, pre64, tau, parents, sh,
-                           cl, red, M, cnt, ch.seed, ch.chain_id, t, Ucur, ph_acc, dbg != nullptr);
+      int fs = FAST_FALLBACK;
+      if (M <= 64)
+        fs = top_set_resample<NT>(W, N, mx, logS, c->sig_thresh, lst, lst_base, lst_cnt, smem + lay.W,
+                                  lay.bcnt - lay.W,
+                                  (uint64_t*)(smem + lay.bcnt), lay.bcnt_bytes, part_cnt, part_tot, parents, sh, cl,
+                                  red, M, cnt, Ucur, ph_acc, dbg != nullptr);
+      PH(20);
+      if (fs != FAST_DONE) {
+        if (fs == FAST_FALLBACK_REGEN) {  // the top-set path used the W area: rebuild step t-1's weights
+          if (prev_mode == MODE_INIT) {
+            gen_weights_init<NT>(cl, K, sh.r_ph, erow(ering, t - 1, K2), W, &mloc, &cloc);
+          } else {
+            gen_weights<NT>(cl, K, I, np_prev, prev_mode, prev_logc, prev_lse, pst, pw, phz,
+                            erow(ering, t - 1, K2), W, &mloc, &cloc);
+          }
+          lds_barrier();
+        }
+        optimal_resample<NT>(W, (uint64_t*)W, N, mx, logS, c->sig_thresh, keys, bcnt, bpos, pre64, tau, parents,
+                             sh, cl, red, M, cnt, ch.seed, ch.chain_id, t, Ucur, ph_acc, dbg != nullptr);
+        if (dbg && tid == 0) ph_acc[21]++;
+      }
       if (dbg && tid == 0) ph_acc[9] += sh.n_sig;
       PH(3);
       int Kk = sh.Kk;
@@ -936,7 +1265,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         // ---- unbiased fallback: M categorical draws from log_weights (:42-47)
         mode = MODE_UNBIASED;
         log_c = 0.0f;
-        const double lmax = (double)key_value(((const uint64_t*)W)[0]);
+        const double lmax = (double)(float)((mx - mx) - logS);  // the largest f32 log-weight
         lds_barrier();  // the sorted keys in the W area are replaced by the regenerated weights
         if (prev_mode == MODE_INIT) {
           gen_weights_init<NT>(cl, K, sh.r_ph, erow(ering, t - 1, K2), W, &mloc, &cloc);
@@ -1082,8 +1411,8 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     for (int n = tid; n < Nmax; n += NT) finalw_out[(size_t)blockIdx.x * Nmax + n] = (n < N) ? W[n] : HYG_NINF;
   }
   if (dbg && tid == 0) {
-    for (int k = 0; k < 23; ++k) dbg[(size_t)blockIdx.x * 24 + k] = ph_acc[k];
-    dbg[(size_t)blockIdx.x * 24 + 23] = (unsigned long long)T;
+    for (int k = 0; k < kPh - 1; ++k) dbg[(size_t)blockIdx.x * kPh + k] = ph_acc[k];
+    dbg[(size_t)blockIdx.x * kPh + kPh - 1] = (unsigned long long)T;
   }
 #undef PH
 }
@@ -1098,30 +1427,38 @@ struct Child {
 __device__ __forceinline__ Child child_of(const ConstLds& cl, int K, int am, int adc, int arc, int adk, int ark,
                                           const Pf3& p, int s) {
   Child x;
-  double2 hc, hk;
+  // c_cont / k_cont: the child's duration continues on the ancestor's
+  // prefetched row; merge (m = 0): case continues on the control row; every
+  // other row is the d = 1 row of the child's own regime
+  bool c_cont, k_cont, merge = false;
   if (s == 0) {
     x.m = am; x.dc = adc + 1; x.rc = arc; x.dk = adk + 1; x.rk = ark;
-    hc = p.c1; hk = p.k1;
+    c_cont = true; k_cont = true;
   } else if (s < K) {
     const int r = (s - 1 < ark) ? s - 1 : s;
     x.m = 0; x.dc = 1; x.rc = r; x.dk = adk + 1; x.rk = ark;
-    hc = cl.hz1[0][r]; hk = p.k1;
+    c_cont = false; k_cont = true;
   } else if (s < 2 * K - 1) {
     const int qq = s - K;
     const int r = (qq < arc) ? qq : qq + 1;
     x.m = 0; x.dc = adc + 1; x.rc = arc; x.dk = 1; x.rk = r;
-    hc = p.c1; hk = cl.hz1[1][r];
+    c_cont = true; k_cont = false;
   } else if (s == 2 * K - 1) {
     const int d = (am == 0) ? adc + 1 : 0;
     x.m = 1; x.dc = d; x.rc = arc; x.dk = d; x.rk = arc;
-    if (am == 0) { hc = p.c1; hk = p.kc; }
-    else { hc = cl.hz1[0][arc]; hk = cl.hz1[1][arc]; }
+    merge = am == 0;
+    c_cont = merge; k_cont = false;
   } else {
     const int j = s - 2 * K, i = j / K, jj = j - i * K;
     x.m = (i == jj); x.dc = 1; x.rc = i; x.dk = 1; x.rk = jj;
-    hc = cl.hz1[0][i]; hk = cl.hz1[1][jj];
+    c_cont = false; k_cont = false;
   }
-  x.h.lrc = hc.x; x.h.l1c = hc.y; x.h.lrk = hk.x; x.h.l1k = hk.y;
+  // value selects (a select of addresses would put p in scratch memory)
+  const double2 h1c = cl.hz1[0][x.rc], h1k = cl.hz1[1][x.rk];
+  x.h.lrc = c_cont ? p.c1.x : h1c.x;
+  x.h.l1c = c_cont ? p.c1.y : h1c.y;
+  x.h.lrk = merge ? p.kc.x : (k_cont ? p.k1.x : h1k.x);
+  x.h.l1k = merge ? p.kc.y : (k_cont ? p.k1.y : h1k.y);
   return x;
 }
 // false when tg_trans(x -> next) selects a constant -inf branch whatever the
@@ -1172,12 +1509,12 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   load_consts(cl, c, md);
   if (tid == 0) sh.status = HYG_OK;
   unsigned long long* ph_acc = sh.ph;
-  if (tid < 24) ph_acc[tid] = 0;
+  if (tid < kPh) ph_acc[tid] = 0;
 #define BPH(k)                                                     \
   if (dbg && tid == 0) {                                           \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-    ph_acc[k] += now_ - ph_acc[23];                                \
-    ph_acc[23] = now_;                                             \
+    ph_acc[k] += now_ - ph_acc[kPh - 1];                                \
+    ph_acc[kPh - 1] = now_;                                             \
   }
   // Records are read ahead in two stages: step t consumes record t from LDS,
   // stores record t-1 (read during step t+1) with its hazard rows (issued at
@@ -1214,7 +1551,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     if (bi > 0) load_eblock(ering, Ech, bi - 1, T, K2, NT);
   }
   lds_barrier();
-  if (dbg && tid == 0) ph_acc[23] = __builtin_amdgcn_s_memtime();
+  if (dbg && tid == 0) ph_acc[kPh - 1] = __builtin_amdgcn_s_memtime();
 
   for (int t = T - 1; t >= 0; --t) {
     // ---- regenerate the particles of step t from its record (in LDS)
@@ -1532,8 +1869,8 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   lds_barrier();
   if (tid == 0 && status_out) status_out[blockIdx.x] = sh.status;
   if (dbg && tid == 0) {
-    for (int k = 0; k < 23; ++k) dbg[(size_t)blockIdx.x * 24 + k] = ph_acc[k];
-    dbg[(size_t)blockIdx.x * 24 + 23] = (unsigned long long)T;
+    for (int k = 0; k < kPh - 1; ++k) dbg[(size_t)blockIdx.x * kPh + k] = ph_acc[k];
+    dbg[(size_t)blockIdx.x * kPh + kPh - 1] = (unsigned long long)T;
   }
 #undef BPH
 }
@@ -1611,22 +1948,22 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
     return HYG_EDEVICE;
   unsigned long long* dbg = nullptr;
   static const bool want_dbg = getenv("HYG_DEBUG_PHASES") != nullptr;
-  if (want_dbg) (void)hipMalloc((void**)&dbg, sizeof(unsigned long long) * 24 * n_chains);
-  if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * 24 * n_chains, s);
+  if (want_dbg) (void)hipMalloc((void**)&dbg, sizeof(unsigned long long) * kPh * n_chains);
+  if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * kPh * n_chains, s);
   ev_record(1, false, s);
   hipLaunchKernelGGL(tg_forward_kernel<NT>, dim3(n_chains), dim3(NT), lf.total, s, md, chains_dev, E, ws,
                      out.status, out.log_z, out.final_log_weights, lf, dbg);
   ev_record(1, true, s);
   if (hipGetLastError() != hipSuccess) return HYG_EDEVICE;
   if (dbg) {
-    std::vector<unsigned long long> h((size_t)24 * n_chains);
+    std::vector<unsigned long long> h((size_t)kPh * n_chains);
     (void)hipStreamSynchronize(s);
     (void)hipMemcpy(h.data(), dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
     (void)hipFree(dbg);
-    unsigned long long tot[24] = {0};
+    unsigned long long tot[kPh] = {0};
     for (int i = 0; i < n_chains; ++i)
-      for (int k = 0; k < 24; ++k) tot[k] += h[(size_t)i * 24 + k];
-    const double steps = (double)tot[23];
+      for (int k = 0; k < kPh; ++k) tot[k] += h[(size_t)i * kPh + k];
+    const double steps = (double)tot[kPh - 1];
     fprintf(stderr, "[hyg phases NT=%d] chains=%d steps=%.0f cycles/step:", NT, n_chains, steps);
     const char* nm[9] = {"top", "lse", "compact", "resample", "fallback", "gather", "wmax", "wgen", "wstore"};
     double sum = 0;
@@ -1638,8 +1975,13 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
             tot[9] / (steps - tot[10]), 0.0);
     fprintf(stderr, " | lse loop=%.0f lse reduce=%.0f", tot[12] / steps, tot[11] / steps);
     const double opt = steps - tot[10];
-    fprintf(stderr, " | per optimal step: hist=%.0f bscan=%.0f scatter=%.0f bsort=%.0f scan=%.0f kloop=%.0f systematic=%.0f\n",
-            tot[17] / opt, tot[18] / opt, tot[19] / opt, tot[13] / opt, tot[14] / opt, tot[15] / opt, tot[16] / opt);
+    fprintf(stderr, " | topset: compact=%.0f mass=%.0f gatherA=%.0f sort=%.0f prefix=%.0f kloop_sys=%.0f",
+            tot[24] / opt, tot[25] / opt, tot[26] / opt, tot[27] / opt, tot[28] / opt, tot[29] / opt);
+    fprintf(stderr, " | per optimal step: topset=%.0f fallbacks=%.4f | per fallback: hist=%.0f bscan=%.0f scatter=%.0f "
+            "bsort=%.0f scan=%.0f kloop=%.0f systematic=%.0f\n", tot[20] / opt, tot[21] / opt,
+            tot[17] / (tot[21] + 1e-9), tot[18] / (tot[21] + 1e-9), tot[19] / (tot[21] + 1e-9),
+            tot[13] / (tot[21] + 1e-9), tot[14] / (tot[21] + 1e-9), tot[15] / (tot[21] + 1e-9),
+            tot[16] / (tot[21] + 1e-9));
   }
   return HYG_OK;
 }
@@ -1655,22 +1997,22 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
     return HYG_EDEVICE;
   static const bool want_dbg = getenv("HYG_DEBUG_PHASES") != nullptr;
   unsigned long long* dbgb = nullptr;
-  if (want_dbg) (void)hipMalloc((void**)&dbgb, sizeof(unsigned long long) * 24 * n_chains);
-  if (dbgb) (void)hipMemsetAsync(dbgb, 0, sizeof(unsigned long long) * 24 * n_chains, s);
+  if (want_dbg) (void)hipMalloc((void**)&dbgb, sizeof(unsigned long long) * kPh * n_chains);
+  if (dbgb) (void)hipMemsetAsync(dbgb, 0, sizeof(unsigned long long) * kPh * n_chains, s);
   ev_record(2, false, s);
   hipLaunchKernelGGL(tg_backward_kernel<NT>, dim3(n_chains), dim3(NT), lb.total, s, md, chains_dev, E,
                      (const uint8_t*)ws, (const int32_t*)out.status, out.merged, out.control, out.kase,
                      out.split_probs, out.regime_probs, out.status, lb, dbgb);
   ev_record(2, true, s);
   if (dbgb) {
-    std::vector<unsigned long long> h((size_t)24 * n_chains);
+    std::vector<unsigned long long> h((size_t)kPh * n_chains);
     (void)hipStreamSynchronize(s);
     (void)hipMemcpy(h.data(), dbgb, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
     (void)hipFree(dbgb);
-    unsigned long long tot[24] = {0};
+    unsigned long long tot[kPh] = {0};
     for (int i = 0; i < n_chains; ++i)
-      for (int k = 0; k < 24; ++k) tot[k] += h[(size_t)i * 24 + k];
-    const double steps = (double)tot[23];
+      for (int k = 0; k < kPh; ++k) tot[k] += h[(size_t)i * kPh + k];
+    const double steps = (double)tot[kPh - 1];
     const char* nm[7] = {"gen", "issue", "dedupe", "list", "wave0", "tail", "traj"};
     fprintf(stderr, "[hyg backward phases NT=%d] cycles/step:", NT);
     double sum = 0;

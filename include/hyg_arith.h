@@ -386,7 +386,10 @@ HYG_HD hyg_ph4 hyg_philox4x64(uint64_t c0, uint64_t c1, uint64_t c2, uint64_t c3
 /* 64 random bits number `index` of (stream, step) for chain (seed, chain_id). */
 HYG_HD uint64_t hyg_rand64(uint64_t seed, uint64_t chain_id, uint32_t stream, uint64_t step, uint64_t index) {
   const hyg_ph4 r = hyg_philox4x64((uint64_t)stream, step, index >> 2, 0, seed, chain_id);
-  return r.v[index & 3];
+  /* value selects, not r.v[index & 3]: a dynamic index would put r in GPU scratch memory */
+  const unsigned q = (unsigned)(index & 3);
+  const uint64_t lo = (q & 1) ? r.v[1] : r.v[0], hi = (q & 1) ? r.v[3] : r.v[2];
+  return (q & 2) ? hi : lo;
 }
 
 /* f32 uniform on [0, 1) from 24 random bits (exact). */
