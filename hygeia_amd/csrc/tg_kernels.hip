@@ -249,12 +249,14 @@ struct Lay {  // byte offsets into the dynamic LDS
   size_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, red, sh, total;
   size_t bcnt_bytes;
   int npad, nkeys, nt;
+  int topset_r;  // keys per lane of the top-set sort: A holds <= 64 * topset_r per wave
 };
 
 __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT, bool backward) {
   // Sized for 3 workgroups per CU at K = 6, M = 50, NT = 256 (<= 53 KiB each).
   Lay l{};
   l.nt = NT;
+  l.topset_r = 1;
   l.npad = Nmax;
   size_t o = 0;
   l.W = o; o = align_up(o + sizeof(double) * l.npad, 16);
@@ -813,9 +815,10 @@ enum { FAST_DONE = 0, FAST_FALLBACK = 1, FAST_FALLBACK_REGEN = 2 };
     ph[kPh - 1] = now_;                                            \
   }
 
-// log-weight cutoffs below the top weight (nats); the last is sig_thresh
-__device__ __forceinline__ float cut_below_top(int k) {
-  constexpr float x[kNCut - 1] = {8.0f, 12.0f, 16.0f, 20.0f, 25.0f, 32.0f, 45.0f};
+// cutoffs of the top set in W - mx (nats below the largest weight); the last
+// set (k = kNCut - 1) is the whole candidate list (W - mx >= sig_thresh)
+__device__ __forceinline__ double cut_below_top(int k) {
+  constexpr double x[kNCut - 1] = {14.0, 17.0, 20.0, 23.0, 26.0, 30.0, 36.0};
   return x[k];
 }
 
@@ -875,7 +878,7 @@ struct Bitonic {
 // Sort A (nA keys in srt[]), exact prefix masses, the K / log c loop and the
 // systematic draws. scr: the W + key areas (W is overwritten).
 template <int NT, int R>
-__device__ int top_set_finish(uint64_t* srt, int nA, int n_sig, int N, int M, int cnt_fin, const hyg_u192& total,
+__device__ int top_set_finish(uint64_t* srt, int nA, bool hasB, int N, int M, int cnt_fin, const hyg_u192& massB,
                               unsigned char* scr, int* parents, Shared& sh, const ConstLds& cl, unsigned char* red,
                               float Usys, unsigned long long* ph, bool timed) {
   const int lane = lane_id();
@@ -900,6 +903,7 @@ __device__ int top_set_finish(uint64_t* srt, int nA, int n_sig, int N, int M, in
   hyg_u192 massA;
   const hyg_u192 ex = block_excl192<NT>(loc, red, &massA);  // its barriers end every sort-buffer read
   hyg_u192* pre = (hyg_u192*)scr;                           // inclusive prefix of sorted position p
+  const hyg_u192 total = hyg_u192_add(massA, massB);         // every significant weight's mass
   hyg_u192 run = ex;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -915,21 +919,25 @@ __device__ int top_set_finish(uint64_t* srt, int nA, int n_sig, int N, int M, in
     float ca = 0.0f;
     hyg_u192 rva = hyg_u192_zero();
     if (a < M && a < N) {
-      if (a < n_sig) {
-        if (a <= nA) rva = hyg_u192_sub(total, a == 0 ? hyg_u192_zero() : pre[a - 1]);
-        else flag = 1;  // prefix outside A
-      }
+      // (positions past the significant weights have zero mass, so R(a) = 0
+      // there; outside the list nothing is significant)
+      if (a <= nA) rva = hyg_u192_sub(total, a == 0 ? hyg_u192_zero() : pre[a - 1]);
+      else if (hasB) flag = 1;  // prefix outside A
       const double rvd = hyg_u192_to_f64(rva);
       const float l2 = (rvd == 0.0) ? HYG_NINFF : (float)hyg_log(rvd);
       ca = cl.logMa[a] - l2;
       if (hyg_isfinitef(ca)) {
-        int lo = 0, hi = nA;  // first p with the predicate false
+        // first p with the predicate false; only min(P, M) matters to the
+        // loop (P >= M ends it), and no weight below sig_thresh can satisfy
+        // it (c < log M + 103.3 there)
+        const int cap = nA < M ? nA : M;
+        int lo = 0, hi = cap;
         while (lo < hi) {
           const int mid = (lo + hi) >> 1;
           if ((float)(ca + key_value(srt[mid])) > 0.0f) lo = mid + 1; else hi = mid;
         }
         Pa = lo;
-        if (lo == nA && nA < n_sig) flag = 1;  // the count may continue below A
+        if (lo == nA && nA < M && hasB) flag = 1;  // the count may continue below A
       } else if (ca > 0.0f) {
         Pa = cnt_fin;
       }
@@ -954,7 +962,7 @@ __device__ int top_set_finish(uint64_t* srt, int nA, int n_sig, int N, int M, in
       hyg_u192 tau = hyg_u192_zero();
       if (lane < L) tau = hyg_u192_add(preK, hyg_ceil_mul_f32(((float)lane + Usys) / (float)L, Rr));
       const hyg_u192 tlast = rdlane192(tau, L > 0 ? L - 1 : 0);
-      if (L > 0 && nA < n_sig && !hyg_u192_ge(massA, tlast)) {
+      if (L > 0 && hasB && !hyg_u192_ge(massA, tlast)) {
         status = FAST_FALLBACK_REGEN;
       } else {
         if (lane < bb) parents[lane] = key_index(srt[lane]);
@@ -981,85 +989,64 @@ __device__ int top_set_finish(uint64_t* srt, int nA, int n_sig, int N, int M, in
 
 // Top-set path of OptimalFiniteState; returns FAST_DONE (parents / Kk /
 // log_c written; log_c infinite -> the caller's unbiased fallback),
-// FAST_FALLBACK (W intact) or FAST_FALLBACK_REGEN (W overwritten).
+// FAST_FALLBACK (W intact) or FAST_FALLBACK_REGEN (W overwritten). The
+// counts of the cutoff sets per wave (part_cnt) were published with the
+// candidate lists before the log-sum-exp reduction.
 template <int NT>
-__device__ int top_set_resample(const double* W, int N, double mx, double logS, float thr, const int* lst, int lb,
-                                int cw,
-                                unsigned char* scr, size_t scr_bytes, uint64_t* srt, size_t srt_bytes, int* part_cnt,
-                                hyg_u192* part_tot, int* parents, Shared& sh, const ConstLds& cl,
-                                unsigned char* red, int M, int cnt_fin, float Usys, unsigned long long* ph,
-                                bool timed) {
+__device__ int top_set_resample(const double* W, int N, double mx, double logS, const int* lst, int lb, int cw,
+                                unsigned char* scr, size_t scr_bytes, uint64_t* srt, size_t srt_bytes,
+                                const int* part_cnt, hyg_u192* part_tot, int* parents, Shared& sh,
+                                const ConstLds& cl, unsigned char* red, int M, int cnt_fin, float Usys,
+                                int rmax, unsigned long long* ph, bool timed) {
   constexpr int NW = NT / 64;
   const int wv = wave_id(), lane = lane_id();
-  const float lwtop = (float)((mx - mx) - logS);  // the largest log-weight
-  float cut[kNCut];
-#pragma unroll
-  for (int k = 0; k < kNCut - 1; ++k) {
-    const float v = lwtop - cut_below_top(k);
-    cut[k] = v > thr ? v : thr;
-  }
-  cut[kNCut - 1] = thr;
-  // ---- 1. per wave, over its list of candidates with W - mx >= sig_thresh:
-  //         exact mass sum of the significant ones and counts per cutoff
-  hyg_u192 ms = hyg_u192_zero();
-  int cc[kNCut];
-#pragma unroll
-  for (int k = 0; k < kNCut; ++k) cc[k] = 0;
-  for (int i = 0; i < cw; i += 64) {
-    const bool v = i + lane < cw;
-    const int n = lst[lb + (v ? i + lane : cw - 1)];
-    const float lw = (float)((W[n] - mx) - logS);
-    const bool sig = v && lw >= thr;
-    const float m = hyg_expf(lw);
-    ms = hyg_u192_add(ms, hyg_fix149f(sig ? m : 0.0f));
-#pragma unroll
-    for (int k = 0; k < kNCut; ++k) cc[k] += (int)__builtin_popcountll(wave_ballot(sig && lw >= cut[k]));
-  }
-  const hyg_u192 wsum = rdlane192(wave_incl192(ms), 63);
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < kNCut; ++k) part_cnt[wv * kNCut + k] = cc[k];
-    part_tot[wv] = wsum;
-  }
-  lds_barrier();
-  TPH(25);
-  // ---- 2. the most inclusive cutoff whose set fits the sort; gather A
-  int ks = -1, nA = 0;
-  int n_sig = 0;
+  // ---- 1. the most inclusive cutoff whose set A fits the sort
+  int ks = -1, nA = 0, nL = 0;
 #pragma unroll
   for (int k = 0; k < kNCut; ++k) {
     int c = 0;
     for (int w = 0; w < NW; ++w) c += part_cnt[w * kNCut + k];
     const int np = (c <= 64 * NW) ? 64 * NW : 128 * NW;
-    if (c <= 128 * NW && (size_t)np * sizeof(hyg_u192) <= scr_bytes && (size_t)np * 8 <= srt_bytes) {
+    if (c <= 64 * NW * rmax && (size_t)np * sizeof(hyg_u192) <= scr_bytes && (size_t)np * 8 <= srt_bytes) {
       ks = k;
       nA = c;
     }
-    n_sig = c;
+    nL = c;
   }
-  if (threadIdx.x == 0) sh.n_sig = n_sig;
+  if (threadIdx.x == 0) sh.n_sig = nL;
   if (ks < 0) return FAST_FALLBACK;  // uniform
-  hyg_u192 total = hyg_u192_zero();
+  const bool hasB = nA < nL;         // list weights outside A (their masses enter the total)
+  const double cutx = (ks == kNCut - 1) ? HYG_NINF : -cut_below_top(ks);
   int off = 0;
-  for (int w = 0; w < NW; ++w) {
-    total = hyg_u192_add(total, part_tot[w]);
-    if (w < wv) off += part_cnt[w * kNCut + ks];
-  }
-  const float cs = cut[ks];
+  for (int w = 0; w < wv; ++w) off += part_cnt[w * kNCut + ks];
+  // ---- 2. gather A's keys; exact mass of the list weights outside A
+  hyg_u192 mb = hyg_u192_zero();
   for (int i = 0; i < cw; i += 64) {
     const bool v = i + lane < cw;
     const int n = lst[lb + (v ? i + lane : cw - 1)];
-    const float lw = (float)((W[n] - mx) - logS);
-    const bool sel = v && lw >= cs;
-    const uint64_t bal = wave_ballot(sel);
-    if (sel) srt[off + lanes_below(bal)] = sort_key(lw, n);
+    const double x = W[n] - mx;
+    const float lw = (float)(x - logS);
+    const bool inA = v && x >= cutx;
+    const uint64_t bal = wave_ballot(inA);
+    if (inA) srt[off + lanes_below(bal)] = sort_key(lw, n);
     off += (int)__builtin_popcountll(bal);
+    if (hasB) {  // uniform; expf(lw) is 0 below sig_thresh
+      const float m = hyg_expf(lw);
+      mb = hyg_u192_add(mb, hyg_fix149f((v && !inA) ? m : 0.0f));
+    }
+  }
+  if (hasB) {
+    const hyg_u192 ws = rdlane192(wave_incl192(mb), 63);
+    if (lane == 0) part_tot[wv] = ws;
   }
   lds_barrier();
+  hyg_u192 massB = hyg_u192_zero();
+  if (hasB)
+    for (int w = 0; w < NW; ++w) massB = hyg_u192_add(massB, part_tot[w]);
   TPH(26);
   if (nA <= 64 * NW)
-    return top_set_finish<NT, 1>(srt, nA, n_sig, N, M, cnt_fin, total, scr, parents, sh, cl, red, Usys, ph, timed);
-  return top_set_finish<NT, 2>(srt, nA, n_sig, N, M, cnt_fin, total, scr, parents, sh, cl, red, Usys, ph, timed);
+    return top_set_finish<NT, 1>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
+  return top_set_finish<NT, 2>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
 }
 #undef TPH
 
@@ -1181,6 +1168,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     int* lst = (int*)keys;
     const int lst_base = wave_id() * (((N + NT - 1) / NT) * 64);
     int lst_cnt = 0;
+    const bool topset = cnt > M && M <= 64;  // this step resamples by the top-set path
     {
       const double cutw = (double)c->sig_thresh;
       for (int b = wave_id() * 64; b < N; b += NT) {
@@ -1194,15 +1182,40 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     }
     double logS;
     {
-      // two independent chains per iteration; fix100(exp(x)) is 0 for x < -70
+      // two independent chains per iteration; fix100(exp(x)) is 0 for x < -70.
+      // Top-set steps also count the list per cutoff (per-lane counters).
       hyg_u128 s0 = hyg_u128_zero(), s1 = hyg_u128_zero();
+      int ccut[kNCut - 1];
+#pragma unroll
+      for (int k = 0; k < kNCut - 1; ++k) ccut[k] = 0;
       int i = lane_id();
       for (; i + 64 < lst_cnt; i += 128) {
         const double x0 = W[lst[lst_base + i]] - mx, x1 = W[lst[lst_base + i + 64]] - mx;
         s0 = hyg_u128_add(s0, hyg_fix100(hyg_exp(x0)));
         s1 = hyg_u128_add(s1, hyg_fix100(hyg_exp(x1)));
+        if (topset) {
+#pragma unroll
+          for (int k = 0; k < kNCut - 1; ++k)
+            ccut[k] += ((x0 >= -cut_below_top(k)) ? 1 : 0) + ((x1 >= -cut_below_top(k)) ? 1 : 0);
+        }
       }
-      if (i < lst_cnt) s0 = hyg_u128_add(s0, hyg_fix100(hyg_exp(W[lst[lst_base + i]] - mx)));
+      if (i < lst_cnt) {
+        const double x0 = W[lst[lst_base + i]] - mx;
+        s0 = hyg_u128_add(s0, hyg_fix100(hyg_exp(x0)));
+        if (topset) {
+#pragma unroll
+          for (int k = 0; k < kNCut - 1; ++k) ccut[k] += (x0 >= -cut_below_top(k)) ? 1 : 0;
+        }
+      }
+      if (topset) {
+#pragma unroll
+        for (int k = 0; k < kNCut - 1; ++k) ccut[k] = wave_sum(ccut[k]);
+        if (lane_id() == 0) {  // read after the reduction's barriers below
+#pragma unroll
+          for (int k = 0; k < kNCut - 1; ++k) part_cnt[wave_id() * kNCut + k] = ccut[k];
+          part_cnt[wave_id() * kNCut + kNCut - 1] = lst_cnt;
+        }
+      }
       const hyg_u128 sacc = hyg_u128_add(s0, s1);
       PH(12);
       const hyg_u128 S = block_sum128<NT>(sacc, red);
@@ -1235,11 +1248,10 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       // ---- OptimalFiniteState (resampling_functions.py:7-52)
       PH(2);
       int fs = FAST_FALLBACK;
-      if (M <= 64)
-        fs = top_set_resample<NT>(W, N, mx, logS, c->sig_thresh, lst, lst_base, lst_cnt, smem + lay.W,
-                                  lay.bcnt - lay.W,
+      if (topset)
+        fs = top_set_resample<NT>(W, N, mx, logS, lst, lst_base, lst_cnt, smem + lay.W, lay.bcnt - lay.W,
                                   (uint64_t*)(smem + lay.bcnt), lay.bcnt_bytes, part_cnt, part_tot, parents, sh, cl,
-                                  red, M, cnt, Ucur, ph_acc, dbg != nullptr);
+                                  red, M, cnt, Ucur, lay.topset_r, ph_acc, dbg != nullptr);
       PH(20);
       if (fs != FAST_DONE) {
         if (fs == FAST_FALLBACK_REGEN) {  // the top-set path used the W area: rebuild step t-1's weights
@@ -1940,8 +1952,10 @@ int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* 
 template <int NT>
 static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
                             const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
-  const Lay lf = make_layout(c.K, c.M, c.B, c.Nmax, NT, false);
+  Lay lf = make_layout(c.K, c.M, c.B, c.Nmax, NT, false);
   if (lf.total > 160 * 1024) return HYG_EUNSUPPORTED;
+  static const char* rv = getenv("HYG_TOPSET_R");  // tuning: 1 (A <= 64 per wave) or 2
+  if (rv && (atoi(rv) == 1 || atoi(rv) == 2)) lf.topset_r = atoi(rv);
   if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
   if (hipFuncSetAttribute((const void*)tg_forward_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lf.total) != hipSuccess)
