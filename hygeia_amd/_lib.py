@@ -103,7 +103,14 @@ EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy
            "hyg_tg_emission", "hyg_tg_workspace_bytes", "hyg_tg_run_chains", "hyg_tg_run_chain_host",
            "hyg_device_count", "hyg_last_error", "hyg_version", "hyg_set_kernel_timing", "hyg_tg_last_kernel_ms",
            "hyg_sg_params_default", "hyg_sg_model_create", "hyg_sg_model_destroy", "hyg_sg_emission",
-           "hyg_sg_workspace_bytes", "hyg_sg_run_chains", "hyg_sg_run_chain_host")
+           "hyg_sg_workspace_bytes", "hyg_sg_run_chains", "hyg_sg_run_chain_host",
+           "hyg_dmp_site_counts", "hyg_dmp_fdr", "hyg_dmp_weighted_fdr")
+
+
+class DmpGroup(C.Structure):
+    """Mirror of hyg_dmp_group (include/hygeia_amd.h)."""
+
+    _fields_ = [("site_begin", C.c_int64), ("n_rows", C.c_int64)]
 
 _lib = None
 
@@ -164,6 +171,15 @@ def load() -> C.CDLL:
     L.hyg_sg_run_chains.argtypes = [vp, C.POINTER(SgChain), i32, vp, vp, sz, i32, vp, vp, vp]
     L.hyg_sg_run_chain_host.restype = C.c_int
     L.hyg_sg_run_chain_host.argtypes = [vp, vp, vp, i32, i32, u64, u64, vp]
+    L.hyg_dmp_site_counts.restype = C.c_int
+    L.hyg_dmp_site_counts.argtypes = [vp, vp, vp, i32, i32, C.POINTER(DmpGroup), C.POINTER(i64), i32, i32, i64, vp,
+                                      vp, vp]
+    L.hyg_dmp_fdr.restype = C.c_int
+    L.hyg_dmp_fdr.argtypes = [vp, i32, i32, i64, i32, C.c_double, C.POINTER(i64), C.POINTER(C.c_double),
+                              C.POINTER(C.c_double), vp]
+    L.hyg_dmp_weighted_fdr.restype = C.c_int
+    L.hyg_dmp_weighted_fdr.argtypes = [vp, i32, i32, i64, i32, C.c_double, vp, vp, vp, C.POINTER(i64),
+                                       C.POINTER(C.c_double), vp]
     L.hyg_version.restype = C.c_char_p
     L.hyg_version.argtypes = []
     _lib = L

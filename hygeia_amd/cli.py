@@ -60,12 +60,12 @@ class FlagError(ValueError):
     pass
 
 
-def parse_flags(argv: Sequence[str]) -> Dict[str, object]:
+def parse_flags(argv: Sequence[str], flags_spec=None) -> Dict[str, object]:
     """absl-style parsing: --name=value, --name value, --bool / --nobool, list
-    flags comma separated, multi flags repeated."""
-    spec = {n: (k, d) for n, k, d, _ in FLAGS_SPEC}
+    flags comma separated, multi flags repeated (FLAGS_SPEC unless given)."""
+    spec = {n: (k, d) for n, k, d, _ in (FLAGS_SPEC if flags_spec is None else flags_spec)}
     out: Dict[str, object] = {}
-    multi: Dict[str, List[int]] = {}
+    multi: Dict[str, List[object]] = {}
     i = 0
     argv = list(argv)
     while i < len(argv):
@@ -111,6 +111,8 @@ def parse_flags(argv: Sequence[str]) -> Dict[str, object]:
                 out[name] = [x for x in val.split(",") if x != ""]
             elif kind == "multi_int":
                 multi.setdefault(name, []).extend(int(x) for x in val.split(","))
+            elif kind == "multi_float":
+                multi.setdefault(name, []).extend(float(x) for x in val.split(","))
             else:
                 out[name] = val
         except ValueError as e:
@@ -270,13 +272,21 @@ def main(argv: Sequence[str] = None) -> int:
         except FlagError as e:
             print(f"FATAL Flags parsing error: {e}", file=sys.stderr)
             return 1
+    if cmd in ("aggregate", "get_dmps"):
+        from . import dmp
+        try:
+            return dmp.aggregate_main(rest) if cmd == "aggregate" else dmp.get_dmps_main(rest)
+        except FlagError as e:
+            print(f"FATAL Flags parsing error: {e}", file=sys.stderr)
+            return 1
     if cmd in ("version", "-v", "--version"):
         from . import _lib
         print("Hygeia version {} ({})".format(os.environ.get("HYGEIA_VERSION", ""),
                                               _lib.load().hyg_version().decode()))
         return 0
     if cmd in ("help", "-h", "--help"):
-        print("Usage: hygeia [command] [arguments...]\n  infer  - Run inference on two groups (MI355X)")
+        print("Usage: hygeia [command] [arguments...]\n  infer     - Run inference on two groups (MI355X)\n"
+              "  aggregate - Aggregate results\n  get_dmps  - Get DMPs (Differentially Methylated Positions)")
         return 0
     if cmd in COMMANDS.split():
         print(f"Error: '{cmd}' is not part of the MI355X inference path; use the reference pipeline step",

@@ -14,6 +14,7 @@
 #include "../../include/hyg_sg_model.h"
 #include "sg_common.h"
 #include "tg_common.h"
+#include "dmp_common.h"
 
 using namespace hyg;
 
@@ -507,6 +508,163 @@ int hyg_sg_run_chain_host(const hyg_sg_model* m, const uint16_t* meth, const uin
     return fail(HYG_EDEVICE, "copy failed");
   if (st == HYG_ENOMEM) return fail(st, "pending smoothing times exceeded psi_capacity");
   if (st != HYG_OK) return fail(st, "all particle weights became -inf");
+  return HYG_OK;
+}
+
+}  // extern "C"
+
+// ================================================ aggregation and DMPs
+namespace {
+
+struct DevBuf {  // RAII device allocation
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  bool alloc(size_t n) { return hipMalloc(&p, n ? n : 1) == hipSuccess; }
+};
+
+// FDR_procedure's statistics in numpy's sorted order (ascending t = 1 - c/P,
+// i.e. descending c), as runs of hist[c] equal values.
+struct SortedStats {
+  const std::vector<uint32_t>& hist;
+  int P;
+  double value(int c) const { return 1.0 - (double)c / (double)P; }
+};
+
+}  // namespace
+
+extern "C" {
+
+int hyg_dmp_site_counts(const int16_t* merged, const int16_t* control, const int16_t* kase, int32_t B, int32_t K,
+                        const hyg_dmp_group* groups, const int64_t* block_rows, int32_t n_groups, int32_t n_seeds,
+                        int64_t n_sites, int32_t* counts, int32_t* pairs, void* stream) {
+  if (!merged || !control || !kase || !counts || B < 1 || K < 1 || K > HYG_KMAX || n_groups < 0 || n_seeds < 1 ||
+      (n_groups > 0 && (!groups || !block_rows)))
+    return fail(HYG_EINVAL, "hyg_dmp_site_counts: invalid arguments");
+  if (!have_device()) return fail(HYG_EDEVICE, "no HIP device");
+  if (n_groups == 0) return HYG_OK;
+  std::vector<int64_t> row0(n_groups + 1), site(n_groups);
+  row0[0] = 0;
+  for (int g = 0; g < n_groups; ++g) {
+    if (groups[g].n_rows < 0 || groups[g].site_begin < 0 || groups[g].site_begin + groups[g].n_rows > n_sites)
+      return fail(HYG_EINVAL, "hyg_dmp_site_counts: group outside [0, n_sites)");
+    row0[g + 1] = row0[g] + groups[g].n_rows;
+    site[g] = groups[g].site_begin;
+  }
+  DevBuf d_row0, d_site, d_blk;
+  const size_t nb = (size_t)n_groups * n_seeds;
+  if (!d_row0.alloc(sizeof(int64_t) * (n_groups + 1)) || !d_site.alloc(sizeof(int64_t) * n_groups) ||
+      !d_blk.alloc(sizeof(int64_t) * nb))
+    return fail(HYG_ENOMEM, "device allocation failed");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(d_row0.p, row0.data(), sizeof(int64_t) * (n_groups + 1), hipMemcpyHostToDevice, s) ||
+      hipMemcpyAsync(d_site.p, site.data(), sizeof(int64_t) * n_groups, hipMemcpyHostToDevice, s) ||
+      hipMemcpyAsync(d_blk.p, block_rows, sizeof(int64_t) * nb, hipMemcpyHostToDevice, s))
+    return fail(HYG_EDEVICE, "copy failed");
+  if (launch_dmp_site_counts(merged, control, kase, B, K, (const int64_t*)d_row0.p, (const int64_t*)d_site.p,
+                             (const int64_t*)d_blk.p, n_groups, n_seeds, row0[n_groups], counts, pairs, stream))
+    return fail(HYG_EDEVICE, "dmp_site_counts launch failed");
+  // the descriptors are freed on return: wait for the kernel
+  if (hipStreamSynchronize(s) != hipSuccess) return fail(HYG_EDEVICE, "kernel execution failed");
+  return HYG_OK;
+}
+
+int hyg_dmp_fdr(const int32_t* counts, int32_t stride, int32_t column, int64_t n, int32_t P, double thr, int64_t* k,
+                double* q_k, double* threshold, void* stream) {
+  if (!counts || !k || !q_k || !threshold || n < 1 || P < 1 || stride < 1 || column < 0 || column >= stride)
+    return fail(HYG_EINVAL, "hyg_dmp_fdr: invalid arguments");
+  if (!have_device()) return fail(HYG_EDEVICE, "no HIP device");
+  hipStream_t s = (hipStream_t)stream;
+  DevBuf d_hist, d_bad;
+  if (!d_hist.alloc(sizeof(uint32_t) * (P + 1)) || !d_bad.alloc(sizeof(int32_t)))
+    return fail(HYG_ENOMEM, "device allocation failed");
+  if (hipMemsetAsync(d_hist.p, 0, sizeof(uint32_t) * (P + 1), s) || hipMemsetAsync(d_bad.p, 0, 4, s))
+    return fail(HYG_EDEVICE, "memset failed");
+  if (launch_dmp_hist(counts, stride, column, n, P, (uint32_t*)d_hist.p, (int32_t*)d_bad.p, stream))
+    return fail(HYG_EDEVICE, "dmp_hist launch failed");
+  std::vector<uint32_t> hist(P + 1);
+  int32_t bad = 0;
+  if (hipMemcpyAsync(hist.data(), d_hist.p, sizeof(uint32_t) * (P + 1), hipMemcpyDeviceToHost, s) ||
+      hipMemcpyAsync(&bad, d_bad.p, 4, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
+    return fail(HYG_EDEVICE, "kernel execution failed");
+  if (bad) return fail(HYG_EINVAL, "hyg_dmp_fdr: a count lies outside [0, n_particles]");
+  const SortedStats st{hist, P};
+  int cmax = P;
+  while (cmax >= 0 && hist[cmax] == 0) --cmax;
+  // ordered_test_statistics[0] (:4) is the statistic of the largest count
+  if (thr < st.value(cmax)) {  // (:8-9)
+    *k = 0; *q_k = 0.0; *threshold = 0.0;
+    return HYG_OK;
+  }
+  // Qs = 1./linspace(1, n, n) * cumsum(ordered) (:5-6), numpy's sequential
+  // float64 cumsum; s = sum(Qs <= thr) (:7)
+  double acc = 0.0, q_last = 0.0, q_s1 = 0.0;
+  int64_t i = 0, cnt = 0;
+  for (int c = cmax; c >= 0; --c) {
+    const double v = st.value(c);
+    for (uint32_t r = 0; r < hist[c]; ++r, ++i) {
+      acc = (i == 0) ? v : acc + v;
+      const double q = (1.0 / (double)(i + 1)) * acc;
+      cnt += (q <= thr) ? 1 : 0;
+      q_last = q;
+    }
+  }
+  const int64_t sel = cnt;
+  if (sel == n) {  // `s == test_statistics.shape` (:10-11)
+    *k = n; *q_k = q_last; *threshold = 1.01;
+    return HYG_OK;
+  }
+  // Qs[s-1] and ordered[s] (:12): replay up to position s
+  acc = 0.0; i = 0;
+  double ord_s = 0.0;
+  bool done = false;
+  for (int c = cmax; c >= 0 && !done; --c) {
+    const double v = st.value(c);
+    for (uint32_t r = 0; r < hist[c]; ++r, ++i) {
+      if (i == sel) { ord_s = v; done = true; break; }
+      acc = (i == 0) ? v : acc + v;
+      q_s1 = (1.0 / (double)(i + 1)) * acc;
+    }
+  }
+  *k = sel; *q_k = q_s1; *threshold = ord_s;
+  return HYG_OK;
+}
+
+int hyg_dmp_weighted_fdr(const int32_t* counts, int32_t stride, int32_t column, int64_t n, int32_t P, double thr,
+                         const double* w_fp, const double* w_fn, int64_t* ranked, int64_t* s_out, double* n_sum,
+                         void* stream) {
+  if (!counts || !w_fp || !w_fn || !ranked || !s_out || !n_sum || n < 1 || n > 0x7fffffffll || P < 1 ||
+      stride < 1 || column < 0 || column >= stride)
+    return fail(HYG_EINVAL, "hyg_dmp_weighted_fdr: invalid arguments");
+  if (!have_device()) return fail(HYG_EDEVICE, "no HIP device");
+  hipStream_t s = (hipStream_t)stream;
+  DevBuf d_keys, d_vals, d_exc, d_tmp, d_er;
+  if (!d_keys.alloc(8 * (size_t)n) || !d_vals.alloc(4 * (size_t)n) || !d_exc.alloc(8 * (size_t)n) ||
+      !d_tmp.alloc(radix_temp_bytes(n)) || !d_er.alloc(8 * (size_t)n))
+    return fail(HYG_ENOMEM, "device allocation failed");
+  if (launch_dmp_rank(counts, stride, column, n, P, thr, w_fp, w_fn, (uint64_t*)d_keys.p, (uint32_t*)d_vals.p,
+                      (double*)d_exc.p, stream))
+    return fail(HYG_EDEVICE, "dmp_rank launch failed");
+  if (radix_sort_pairs((uint64_t*)d_keys.p, (uint32_t*)d_vals.p, n, d_tmp.p, stream))
+    return fail(HYG_EDEVICE, "radix sort launch failed");
+  if (launch_dmp_gather((const uint32_t*)d_vals.p, (const double*)d_exc.p, n, (double*)d_er.p, ranked, stream))
+    return fail(HYG_EDEVICE, "dmp_gather launch failed");
+  std::vector<double> e((size_t)n);
+  if (hipMemcpyAsync(e.data(), d_er.p, 8 * (size_t)n, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
+    return fail(HYG_EDEVICE, "kernel execution failed");
+  // Nsums = np.cumsum(ranked excess rates) (:20), s = sum(Nsums <= 0) (:21)
+  double acc = 0.0;
+  int64_t cnt = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    acc = (i == 0) ? e[0] : acc + e[i];
+    cnt += (acc <= 0.0) ? 1 : 0;
+  }
+  const int64_t last = (cnt == 0) ? n - 1 : cnt - 1;  // Nsums[s - 1]
+  acc = 0.0;
+  for (int64_t i = 0; i <= last; ++i) acc = (i == 0) ? e[0] : acc + e[i];
+  *s_out = cnt;
+  *n_sum = acc;
   return HYG_OK;
 }
 

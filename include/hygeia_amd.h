@@ -219,6 +219,58 @@ int hyg_sg_run_chain_host(const hyg_sg_model* model, const uint16_t* meth, const
                           int32_t n_samples, int32_t n_sites, uint64_t seed, uint64_t chain_id,
                           double* regime_probs);
 
+/* ================================================ aggregation and DMPs
+ * The consumers of the two-group trajectories:
+ *   aggregate_results.py:71-206  per-site means over every seed's trajectories
+ *                                (split_probs = mean(merged == 0), regimes)
+ *   get_dmps.py:46-180           test statistics 1 - #(r_ctrl != r_case) / P
+ *                                (and 1 - #(r_ctrl = i, r_case = j) / P), FDR
+ *                                and weighted-FDR selection, regime frequencies
+ *   multiple_testing.py:3-22     FDR_procedure, weighted_FDR_procedure
+ * on trajectories resident in HBM (the outputs of hyg_tg_run_chains). */
+
+/* One chromosome segment: the same reported (trimmed) rows in every seed's
+ * trajectory block. */
+typedef struct hyg_dmp_group {
+  int64_t site_begin; /* global site index of the first reported row */
+  int64_t n_rows;     /* reported rows */
+} hyg_dmp_group;
+
+/* Per-site counts over the P = B * n_seeds trajectories of a site (device
+ * pointers; host arrays `groups` [n_groups] and `block_rows`
+ * [n_groups][n_seeds] = output row, in merged/control/kase, of the first
+ * reported row of each seed's block):
+ *   counts [n_sites][2 + 2K] int32 = (#(merged == 0), #(r_ctrl != r_case),
+ *                                     #(r_ctrl == r) for r < K, #(r_case == r) for r < K)
+ *   pairs  [n_sites][K][K]   int32 = #(r_ctrl == i and r_case == j), or NULL.
+ * merged [rows][B], control/kase [rows][B][2] (d, r) int16 as hyg_tg_outputs.
+ * Rows of sites outside every group are not written. */
+int hyg_dmp_site_counts(const int16_t* merged, const int16_t* control, const int16_t* kase, int32_t B,
+                        int32_t K, const hyg_dmp_group* groups, const int64_t* block_rows, int32_t n_groups,
+                        int32_t n_seeds, int64_t n_sites, int32_t* counts, int32_t* pairs, void* stream);
+
+/* FDR_procedure(t, fdr_threshold) (multiple_testing.py:3-12) for the
+ * statistics t_i = 1 - c_i / P, c_i = counts[i * stride + column] (device),
+ * 0 <= c_i <= P: the ascending sort is a counting sort by c (device), the
+ * float64 running means np.cumsum(sorted) / (i + 1) are replayed exactly in
+ * numpy's sequential order on the host. Outputs the reference's (k, Q_k,
+ * threshold): (0, 0, 0) when fdr_threshold < min t; (n, Q_n, 1.01) when every
+ * Q_i <= fdr_threshold (the reference's `s == shape` branch). Synchronises. */
+int hyg_dmp_fdr(const int32_t* counts, int32_t stride, int32_t column, int64_t n, int32_t n_particles,
+                double fdr_threshold, int64_t* k, double* q_k, double* threshold, void* stream);
+
+/* weighted_FDR_procedure(t, fdr_threshold, w_fp, w_fn) (multiple_testing.py:14-22)
+ * for the same statistics: ranking computed and sorted on the device (stable
+ * LSD radix sort; the reference's np.argsort is not stable, so ties of the
+ * ranking keep ascending site order here), Nsums = np.cumsum of the ranked
+ * excess error rates replayed exactly on the host. ranked [n] (device,
+ * int64) receives ranking_indices; *s the number selected (ranked[0:s]),
+ * *n_sum = Nsums[s - 1] (Python indexing: the last sum when s = 0).
+ * Synchronises. */
+int hyg_dmp_weighted_fdr(const int32_t* counts, int32_t stride, int32_t column, int64_t n, int32_t n_particles,
+                         double fdr_threshold, const double* w_fp, const double* w_fn, int64_t* ranked,
+                         int64_t* s, double* n_sum, void* stream);
+
 /* Number of visible HIP devices (0 when none: compute calls then fail). */
 int hyg_device_count(void);
 const char* hyg_last_error(void);
