@@ -43,6 +43,15 @@ def bytes_per_unit(s_ctrl: int, s_case: int, K: int, M: int, B: int) -> int:
     return 4 * (s_ctrl + s_case) + 2 * M * 16 + B * 10 + 4 * (1 + 2 * K)
 
 
+def _config_name(args) -> str:
+    """BASELINE.json config the arguments describe (SURVEY.md 8 shorthand)."""
+    if args.K == 12 and args.samples == 50:
+        return "C5"
+    if args.K == 6 and args.samples == 4 and args.seeds == 2:
+        return "C3"
+    return "custom"
+
+
 def cpu_baseline(args, d_host, chains, seconds: float, threads: int):
     """The CPU oracle (oracle/tg_oracle.c, 'port') on `threads` host threads,
     each running emission + filter + backward simulation on a prefix of one
@@ -217,7 +226,7 @@ def main():
         "metric": METRIC, "value": value, "unit": "CpG-sites*seeds/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"C3 two_group {args.sites} CpG (22 chromosomes, 100k segments + 5k buffers), "
+        "config": {"workload": f"{_config_name(args)} two_group {args.sites} CpG (22 chromosomes, 100k segments + 5k buffers), "
                                f"{args.samples}+{args.samples} samples, K={K}, M={M}, B={B}, "
                                f"{args.seeds} seeds per GPU", "chains_per_gpu": len(chains),
                    "global_sites_x_seeds": units * world, "parallelism": f"chains over {world} GPU(s)"},
