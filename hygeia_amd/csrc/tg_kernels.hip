@@ -1841,6 +1841,22 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
       o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
     }
+    if (B <= 64 && wave_id() == 0) {  // trajectory b on lane b of wave 0 (its own X write): means by ballots
+      const int lane = lane_id();
+      const bool v = lane < B;
+      const uint64_t x = v ? X[lane] : 0ull;
+      int myc = __builtin_popcountll(__ballot(v && hyg_st_m(x) == 0));
+      for (int r = 0; r < K; ++r) {
+        const int cc = __builtin_popcountll(__ballot(v && hyg_st_rc(x) == r));
+        const int ck = __builtin_popcountll(__ballot(v && hyg_st_rk(x) == r));
+        myc = (lane == 1 + r) ? cc : ((lane == 1 + K + r) ? ck : myc);
+      }
+      if (lane < 2 * K + 1) {
+        const float vv = (float)myc / (float)B;
+        if (lane == 0) o_split[ch.out_begin + t] = vv;
+        else o_regime[(size_t)(ch.out_begin + t) * K2 + (lane - 1)] = vv;
+      }
+    }
     BPH(6);
     // ---- record t-1 (+ hazard rows) replaces record t once every read of it is done
     lds_barrier();
@@ -1861,7 +1877,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       }
     }
     lds_barrier();
-    if (tid < 2 * K + 1) {
+    if (B > 64 && tid < 2 * K + 1) {
       int cntv = 0;
       for (int b = 0; b < B; ++b) {
         const uint64_t x = X[b];
