@@ -246,7 +246,8 @@ constexpr int kBuckets = 512;  // counting-sort buckets of the resampling sort (
 constexpr int kNCut = 8;       // log-weight cutoffs of the top-set resampling path
 
 struct Lay {  // byte offsets into the dynamic LDS
-  size_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, red, sh, total;
+  size_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, rb, red, sh,
+      total;
   size_t bcnt_bytes;
   int npad, nkeys, nt;
   int topset_r;  // keys per lane of the top-set sort: A holds <= 64 * topset_r per wave
@@ -292,6 +293,7 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
     l.X = o; o = align_up(o + sizeof(uint64_t) * B, 16);
     l.grp = o; o = align_up(o + sizeof(int) * B, 16);
     l.gst = o; o = align_up(o + sizeof(uint64_t) * B, 16);
+    l.rb = o; o = align_up(o + 2 * sizeof(uint64_t) * ((B + 3) / 4) * 4, 16);  // draw bits, two steps
   }
   l.red = o; o = align_up(o + 32 * (NT / 64), 16);
   l.sh = o; o = align_up(o + sizeof(Shared), 16);
@@ -1486,6 +1488,17 @@ __device__ __forceinline__ bool trans_possible(int u, const Child& x, int mn, in
   return lm && lc && lk;
 }
 
+// The random bits of step t's B backward draws, hyg_rand64(seed, chain,
+// BACKWARD, t, b) for b < B (Philox blocks of 4, one lane per block), into
+// rb[0..B); run by one otherwise idle wave one step ahead of their use.
+__device__ __forceinline__ void backward_bits(uint64_t* rb, int B, int t, uint64_t seed, uint64_t chain_id) {
+  const int q = lane_id();
+  if (4 * q < B) {
+    const hyg_ph4 r = hyg_philox4x64((uint64_t)HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)q, 0, seed, chain_id);
+    rb[4 * q + 0] = r.v[0]; rb[4 * q + 1] = r.v[1]; rb[4 * q + 2] = r.v[2]; rb[4 * q + 3] = r.v[3];
+  }
+}
+
 template <int NT>
 __global__ void __launch_bounds__(NT)
 tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
@@ -1512,6 +1525,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   uint64_t* X = (uint64_t*)(smem + lay.X);
   int* grp = (int*)(smem + lay.grp);
   uint64_t* gst = (uint64_t*)(smem + lay.gst);
+  uint64_t* rb = (uint64_t*)(smem + lay.rb);
   unsigned char* red = smem + lay.red;
   Shared& sh = *(Shared*)(smem + lay.sh);
 
@@ -1640,6 +1654,10 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       const int sl = fdiv(n, np, rnp), a = n - sl * np;
       return child_hz(cl, K, P[a], sl, PF[a], md);
     };
+    const int rbs = ((B + 3) / 4) * 4;  // stride of the two draw-bit buffers
+    const bool pre_bits = B <= 64 && NT >= 128;
+    if (pre_bits && t == T - 1 && t >= 1 && wave_id() == NT / 64 - 1)
+      backward_bits(rb + ((t - 1) & 1) * rbs, B, t - 1, ch.seed, ch.chain_id);
     if (t == T - 1) {
       // ---- B draws from the final weights (:383-385)
       const double lmax = block_max<NT>(mloc, red);
@@ -1764,6 +1782,8 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         auto rnd = [&](int b) -> uint64_t {
           return hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
         };
+        if (pre_bits && g == 0 && t >= 1 && wave_id() == NT / 64 - 1)  // next step's bits, while wave 0 draws
+          backward_bits(rb + ((t - 1) & 1) * rbs, B, t - 1, ch.seed, ch.chain_id);
         if (L <= 64 && B <= 64 && c->Nmax >= 192) {
           // ---- one wave: order the list by n, exact masses, scan, draws
           if (wave_id() == 0) {
@@ -1790,7 +1810,8 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
             // lane b draws for trajectory b: first list entry with cdf > target
             if (lane < B && grp[lane] == g) {
-              const hyg_u128 tb = hyg_scale_target(rnd(lane), total);
+              const uint64_t bits = pre_bits ? rb[(t & 1) * rbs + lane] : rnd(lane);  // = hyg_rand64(.., t, lane)
+              const hyg_u128 tb = hyg_scale_target(bits, total);
               int lo = 0, hi = L - 1;
               while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
