@@ -5,7 +5,13 @@ runs one R process per (sample group, chromosome); one "step" = emission table
 + SMC / optimal resampling / online marginal smoothing of every chain, counts
 resident in HBM. Prints one JSON line in bench.py's format (units = CpG sites).
 
-    python tools/bench_sg.py [--sites N] [--steps K] [--warmup W]
+    python tools/bench_sg.py [--sites N] [--steps K] [--warmup W] [--per-sample]
+
+--per-sample runs the single-group pipeline's granularity instead
+(modules/single_group/3_estimate_regimes.nf: one process per (case_id,
+chromosome), one sample per chain): samples x 22 chains of S = 1, units = CpG
+sites x samples. The default is the joint S-sample chain per chromosome (the
+two-group pipeline's step 2 on the control group, 2_estimate_parameters_and_regimes.nf).
 """
 from __future__ import annotations
 
@@ -75,11 +81,22 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--per-sample", action="store_true", help="one chain per (sample, chromosome), S = 1")
     args = ap.parse_args()
 
     import torch
 
     from hygeia_amd import _lib, synthetic
+
+    # the chain kernel runs for minutes: a heartbeat keeps the run visibly alive
+    t_start = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(20)
+            print(f"[bench_sg] alive {time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
 
     dev = torch.device("cuda", 0)
     L = _lib.load()
@@ -89,7 +106,17 @@ def main():
     del d["meth_case"], d["tot_case"]
     sizes = synthetic.chromosome_sizes(args.sites)
     begins = np.concatenate([[0], np.cumsum(sizes)[:-1]])
-    chains = sorted([(int(b), int(n), i) for i, (b, n) in enumerate(zip(begins, sizes))], key=lambda c: -c[1])
+    n_rows = args.sites  # rows of the emission / output tables
+    if args.per_sample:  # sample-major [S][T][1]: sample s's chain rows start at s * T
+        meth = meth.t().contiguous().reshape(S * args.sites, 1)
+        tot = tot.t().contiguous().reshape(S * args.sites, 1)
+        n_rows = S * args.sites
+        cl = [(int(s * args.sites + b), int(n), s * 22 + i) for s in range(S)
+              for i, (b, n) in enumerate(zip(begins, sizes))]
+        S = 1
+    else:
+        cl = [(int(b), int(n), i) for i, (b, n) in enumerate(zip(begins, sizes))]
+    chains = sorted(cl, key=lambda c: -c[1])
     arr = (_lib.SgChain * len(chains))()
     for i, (b, n, ci) in enumerate(chains):
         arr[i].site_begin, arr[i].n_sites, arr[i].seed, arr[i].chain_id, arr[i].out_begin = b, n, 1, ci, b
@@ -102,8 +129,8 @@ def main():
     _lib.check(L.hyg_sg_model_create(C.byref(p), max_reads, int(max(sizes)), C.byref(h)))
     wsb = int(L.hyg_sg_workspace_bytes(h, len(chains), args.psi_capacity))
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-    E = torch.empty((args.sites, K), dtype=torch.float64, device=dev)
-    probs = torch.empty((args.sites, K), dtype=torch.float64, device=dev)
+    E = torch.empty((n_rows, K), dtype=torch.float64, device=dev)
+    probs = torch.empty((n_rows, K), dtype=torch.float64, device=dev)
     st = torch.zeros(len(chains), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
@@ -112,7 +139,7 @@ def main():
 
     def step(timed):
         ev[0].record(stream)
-        _lib.check(L.hyg_sg_emission(h, meth.data_ptr(), tot.data_ptr(), S, args.sites, E.data_ptr(), sp))
+        _lib.check(L.hyg_sg_emission(h, meth.data_ptr(), tot.data_ptr(), S, n_rows, E.data_ptr(), sp))
         ev[1].record(stream)
         _lib.check(L.hyg_sg_run_chains(h, arr, len(chains), E.data_ptr(), ws.data_ptr(), wsb, args.psi_capacity,
                                        probs.data_ptr(), st.data_ptr(), sp))
@@ -146,16 +173,20 @@ def main():
     ms = dt * 1000.0 / args.steps
     kavg = kms / args.steps
     bps = bytes_per_site(S, K)
+    units = n_rows  # CpG sites (joint chains) or sites x samples (per-sample chains)
     line = {
-        "metric": "CpG sites/sec through SMC + online smoothing (single group)", "value": args.sites / (ms / 1000.0),
-        "unit": "CpG-sites/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "metric": "CpG sites/sec through SMC + online smoothing (single group)", "value": units / (ms / 1000.0),
+        "unit": "CpG-site-samples/s" if args.per_sample else "CpG-sites/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"C2 single_group {args.sites} CpG, 22 chromosome chains, {S} samples, K={K}, "
-                               f"N_max=250, epsilon=0.01, 1 seed, coverage {args.coverage}",
+        "config": {"workload": (f"C2 single_group {args.sites} CpG x {args.samples} samples, one chain per "
+                                f"(sample, chromosome) = {len(chains)} chains of 1 sample" if args.per_sample else
+                                f"C2 single_group {args.sites} CpG, 22 chromosome chains, {S} samples jointly")
+                               + f", K={K}, N_max=250, epsilon=0.01, 1 seed, coverage {args.coverage}",
                    "chains": len(chains), "longest_chain": int(max(sizes)), "parallelism": "chains on 1 GPU"},
         "roofline": {"bound": "hbm", "kernel": "sg_chain_kernel",
-                     "achieved": bps * args.sites / (kavg[1] / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": bps * args.sites / (kavg[1] / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                     "achieved": bps * units / (kavg[1] / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": bps * units / (kavg[1] / 1000.0) / 1e9 / HBM_PEAK_GBS,
                      "traffic": None, "bytes_per_unit": bps,
                      "kernel_ms": {"sg_emission_kernel": float(kavg[0]), "sg_chain_kernel": float(kavg[1])},
                      "us_per_step_longest_chain": float(kavg[1] * 1000.0 / max(sizes))},
@@ -163,6 +194,7 @@ def main():
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(meth.cpu().numpy().view(np.uint16), tot.cpu().numpy().view(np.uint16),
                                             chains, p, args.cpu_seconds, args.cpu_threads)
+        line["cpu_baseline"]["unit"] = line["unit"]
     L.hyg_sg_model_destroy(h)
     print(json.dumps(line), flush=True)
 
