@@ -88,6 +88,19 @@ class SgParams(C.Structure):
     ]
 
 
+class SgPeParams(C.Structure):
+    """Mirror of hyg_sg_pe_params (include/hygeia_amd.h)."""
+
+    _fields_ = [
+        ("use_adam", C.c_int32),
+        ("normalise_gradients", C.c_int32),
+        ("n_steps_without_update", C.c_int32),
+        ("_pad", C.c_int32),
+        ("learning_rate_exponent", C.c_double),
+        ("learning_rate_factor", C.c_double),
+    ]
+
+
 class SgChain(C.Structure):
     _fields_ = [
         ("site_begin", C.c_int64),
@@ -104,6 +117,8 @@ EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy
            "hyg_device_count", "hyg_last_error", "hyg_version", "hyg_set_kernel_timing", "hyg_tg_last_kernel_ms",
            "hyg_sg_params_default", "hyg_sg_model_create", "hyg_sg_model_destroy", "hyg_sg_emission",
            "hyg_sg_workspace_bytes", "hyg_sg_run_chains", "hyg_sg_run_chain_host",
+           "hyg_sg_pe_params_default", "hyg_sg_pe_theta_rows", "hyg_sg_pe_workspace_bytes", "hyg_sg_run_chains_pe",
+           "hyg_sg_run_chain_host_pe",
            "hyg_dmp_site_counts", "hyg_dmp_fdr", "hyg_dmp_weighted_fdr")
 
 
@@ -171,6 +186,17 @@ def load() -> C.CDLL:
     L.hyg_sg_run_chains.argtypes = [vp, C.POINTER(SgChain), i32, vp, vp, sz, i32, vp, vp, vp]
     L.hyg_sg_run_chain_host.restype = C.c_int
     L.hyg_sg_run_chain_host.argtypes = [vp, vp, vp, i32, i32, u64, u64, vp]
+    L.hyg_sg_pe_params_default.restype = None
+    L.hyg_sg_pe_params_default.argtypes = [C.POINTER(SgPeParams)]
+    L.hyg_sg_pe_theta_rows.restype = i64
+    L.hyg_sg_pe_theta_rows.argtypes = [C.POINTER(SgChain), i32, i32]
+    L.hyg_sg_pe_workspace_bytes.restype = sz
+    L.hyg_sg_pe_workspace_bytes.argtypes = [vp, C.POINTER(SgChain), i32, i32]
+    L.hyg_sg_run_chains_pe.restype = C.c_int
+    L.hyg_sg_run_chains_pe.argtypes = [vp, C.POINTER(SgPeParams), C.POINTER(SgChain), i32, vp, vp, sz, i32, vp, vp,
+                                       vp, vp]
+    L.hyg_sg_run_chain_host_pe.restype = C.c_int
+    L.hyg_sg_run_chain_host_pe.argtypes = [vp, C.POINTER(SgPeParams), vp, vp, i32, i32, u64, u64, vp, vp]
     L.hyg_dmp_site_counts.restype = C.c_int
     L.hyg_dmp_site_counts.argtypes = [vp, vp, vp, i32, i32, C.POINTER(DmpGroup), C.POINTER(i64), i32, i32, i64, vp,
                                       vp, vp]

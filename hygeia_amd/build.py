@@ -17,7 +17,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libhygeia_amd.so")
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("capi.cpp", "tg_kernels.hip", "sg_kernels.hip", "dmp_kernels.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in ("tg_common.h", "sg_common.h", "dmp_common.h", "hyg_dev.h")] + [
-    os.path.join(ROOT, "include", f) for f in ("hygeia_amd.h", "hyg_arith.h", "hyg_model.h", "hyg_sg_model.h")]
+    os.path.join(ROOT, "include", f) for f in ("hygeia_amd.h", "hyg_arith.h", "hyg_model.h", "hyg_sg_model.h", "hyg_sg_pe.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
          "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt",
@@ -32,14 +32,37 @@ def stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compiles the translation units in parallel (one hipcc each, objects
+    under lib/obj) and links the shared library."""
     if not force and not stale():
         return LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
+    from concurrent.futures import ThreadPoolExecutor
+
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"]
+    objs, cmds = [], []
+    headers = [d for d in DEPS if d not in SOURCES]
+    newest_header = max(os.path.getmtime(h) for h in headers)
+    for src in SOURCES:
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        fresh = (not force and os.path.exists(obj) and
+                 os.path.getmtime(obj) > max(os.path.getmtime(src), newest_header))
+        if not fresh:
+            cmds.append([HIPCC] + cflags + ["-c", src, "-o", obj])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    with ThreadPoolExecutor(max_workers=max(1, min(len(cmds), 8))) as ex:
+        for f in [ex.submit(run, c) for c in cmds]:
+            f.result()
     tmp = LIB + ".tmp"
-    cmd = [HIPCC] + FLAGS + ["-o", tmp] + SOURCES
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
+    run(link)
     os.replace(tmp, LIB)
     return LIB
 

@@ -3,6 +3,7 @@
 // hipcc into hygeia_amd/lib/libhygeia_amd.so together with tg_kernels.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -75,6 +76,7 @@ struct hyg_tg_model {
 
 struct hyg_sg_model {
   hyg_sg_consts c{};
+  hyg_sg_params params{};  // as given (initial theta, kappa) for the estimation path
   int32_t dcap = 0;
   int32_t nmax_reads = 0;
   int32_t max_duration = 0;
@@ -382,6 +384,7 @@ int hyg_sg_model_create(const hyg_sg_params* params, int32_t max_total_reads, in
     delete m;
     return fail(HYG_EUNSUPPORTED, "num_particles_max > 256 (one particle per thread of a workgroup)");
   }
+  m->params = *params;
   m->max_duration = max_duration;
   m->nmax_reads = max_total_reads;
   m->dcap = hyg_sg_hazard_len(&m->c, max_duration + 1);
@@ -457,7 +460,9 @@ int hyg_sg_run_chains(const hyg_sg_model* m, const hyg_sg_chain* chains, int32_t
     cd[i].seed = c.seed;
     cd[i].chain_id = c.chain_id;
     cd[i].T = c.n_sites;
-    cd[i].pad = 0;
+    cd[i].rcap = 0;
+    cd[i].pe_offset = 0;
+    cd[i].theta_row = 0;
     off += per;
   }
   uint8_t* ws = (uint8_t*)workspace;
@@ -507,6 +512,163 @@ int hyg_sg_run_chain_host(const hyg_sg_model* m, const uint16_t* meth, const uin
   if (hipMemcpy(regime_probs, b_p.p, sizeof(double) * T * K, hipMemcpyDeviceToHost) != hipSuccess)
     return fail(HYG_EDEVICE, "copy failed");
   if (st == HYG_ENOMEM) return fail(st, "pending smoothing times exceeded psi_capacity");
+  if (st != HYG_OK) return fail(st, "all particle weights became -inf");
+  return HYG_OK;
+}
+
+// ---- online parameter estimation
+
+void hyg_sg_pe_params_default(hyg_sg_pe_params* pe) {
+  std::memset(pe, 0, sizeof(*pe));
+  // bin/estimate_parameters_and_regimes:130-200 flag defaults
+  pe->use_adam = 1;
+  pe->normalise_gradients = 0;
+  pe->n_steps_without_update = 200;
+  pe->learning_rate_exponent = 0.1;
+  pe->learning_rate_factor = 0.01;
+}
+
+static int sg_pe_rcap(int T) { return T + 1 < HYG_SGPE_DCAP ? T + 1 : HYG_SGPE_DCAP; }
+
+int64_t hyg_sg_pe_theta_rows(const hyg_sg_chain* chains, int32_t n_chains, int32_t every) {
+  if (!chains || n_chains < 0 || every < 1) return -1;
+  int64_t rows = 0;
+  for (int i = 0; i < n_chains; ++i) rows += hyg_sgpe_theta_rows(chains[i].n_sites, every);
+  return rows;
+}
+
+size_t hyg_sg_pe_workspace_bytes(const hyg_sg_model* m, const hyg_sg_chain* chains, int32_t n_chains,
+                                 int32_t psi_capacity) {
+  if (!m || !chains || n_chains < 0 || psi_capacity < 0) return 0;
+  size_t b = hyg_sg_workspace_bytes(m, n_chains, psi_capacity);
+  for (int i = 0; i < n_chains; ++i) b += sg_pe_region_bytes(m->c.K, sg_pe_rcap(std::max(chains[i].n_sites, 1)));
+  return b;
+}
+
+int hyg_sg_run_chains_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, const hyg_sg_chain* chains,
+                         int32_t n_chains, const double* E, void* workspace, size_t workspace_bytes,
+                         int32_t psi_capacity, double* regime_probs, double* theta_out, int32_t* status,
+                         void* stream) {
+  if (!m || !pe || !chains || !E || !workspace || !regime_probs || !theta_out) return fail(HYG_EINVAL, "null argument");
+  if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (n_chains <= 0) return HYG_OK;
+  if (psi_capacity < 0 || psi_capacity > (1 << 24)) return fail(HYG_EINVAL, "psi_capacity out of range");
+  hyg_sgpe_consts pc{};
+  int rc = hyg_sgpe_consts_make(&m->params, pe, &pc);
+  if (rc == HYG_EUNSUPPORTED) return fail(rc, "parameter estimation needs is_kappa_fixed (the pipeline default)");
+  if (rc != HYG_OK) return fail(rc, "invalid parameter-estimation settings");
+  const int cap = psi_capacity ? psi_capacity : kSgPsiCapDefault;
+  if (workspace_bytes < hyg_sg_pe_workspace_bytes(m, chains, n_chains, psi_capacity))
+    return fail(HYG_EINVAL, "workspace too small (see hyg_sg_pe_workspace_bytes)");
+  const int K = m->c.K, dim = K * K;
+  std::vector<SgChainDev> cd(n_chains);
+  size_t off = sg_header_bytes(n_chains);
+  const size_t per = sg_chain_ws_bytes(K, cap);
+  size_t pe_off = off + per * (size_t)n_chains;
+  int64_t row = 0, max_rows = 1;
+  int max_rcap = 1;
+  for (int i = 0; i < n_chains; ++i) {
+    const hyg_sg_chain& c = chains[i];
+    if (c.n_sites < 1) return fail(HYG_EINVAL, "chain with no sites");
+    if (c.n_sites > m->max_duration) return fail(HYG_EINVAL, "chain longer than the model's max_duration");
+    if (c.site_begin < 0 || c.out_begin < 0) return fail(HYG_EINVAL, "negative chain offset");
+    cd[i].site_begin = c.site_begin;
+    cd[i].out_begin = c.out_begin;
+    cd[i].psi_offset = (int64_t)off;
+    cd[i].seed = c.seed;
+    cd[i].chain_id = c.chain_id;
+    cd[i].T = c.n_sites;
+    cd[i].rcap = sg_pe_rcap(c.n_sites);
+    cd[i].pe_offset = (int64_t)pe_off;
+    cd[i].theta_row = row;
+    const int64_t nr = hyg_sgpe_theta_rows(c.n_sites, pc.every);
+    row += nr;
+    max_rows = std::max(max_rows, nr);
+    max_rcap = std::max(max_rcap, cd[i].rcap);
+    off += per;
+    pe_off += sg_pe_region_bytes(K, cd[i].rcap);
+  }
+  // model-level inputs: theta0 [dim] | steps [max_rows] | lgk [K][max_rcap]
+  std::vector<hyg_sgpe_step> steps((size_t)max_rows);
+  hyg_sgpe_steps_fill(pe, (int)max_rows, steps.data());
+  std::vector<double> lgk((size_t)K * max_rcap);
+  hyg_sgpe_lgk_fill(pc.kappa, K, max_rcap, lgk.data());
+  const size_t b_th = sizeof(double) * dim, b_st = sizeof(hyg_sgpe_step) * steps.size(),
+               b_lg = sizeof(double) * lgk.size();
+  std::vector<unsigned char> host(b_th + b_st + b_lg);
+  std::memcpy(host.data(), m->params.theta, b_th);
+  std::memcpy(host.data() + b_th, steps.data(), b_st);
+  std::memcpy(host.data() + b_th + b_st, lgk.data(), b_lg);
+  hipStream_t s = (hipStream_t)stream;
+  void* dbuf = nullptr;
+  if (hipMallocAsync(&dbuf, host.size(), s) != hipSuccess) return fail(HYG_ENOMEM, "device allocation failed");
+  if (hipMemcpyAsync(dbuf, host.data(), host.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipFreeAsync(dbuf, s);
+    return fail(HYG_EDEVICE, "upload failed");
+  }
+  uint8_t* ws = (uint8_t*)workspace;
+  if (hipMemcpyAsync(ws, cd.data(), sizeof(SgChainDev) * n_chains, hipMemcpyHostToDevice, s) != hipSuccess) {
+    (void)hipFreeAsync(dbuf, s);
+    return fail(HYG_EDEVICE, "descriptor upload failed");
+  }
+  SgPeDev pd{};
+  pd.c = pc;
+  pd.theta0 = (const double*)dbuf;
+  pd.steps = (const hyg_sgpe_step*)((unsigned char*)dbuf + b_th);
+  pd.lgk = (const double*)((unsigned char*)dbuf + b_th + b_st);
+  pd.lgk_stride = max_rcap;
+  pd.theta_out = theta_out;
+  int32_t* st = status ? status : (int32_t*)(ws + sizeof(SgChainDev) * n_chains);
+  rc = sg_launch_chains(m->dev(), m->c, (const SgChainDev*)ws, n_chains, E, ws, cap, regime_probs, st, stream, &pd);
+  (void)hipFreeAsync(dbuf, s);
+  if (rc == HYG_EUNSUPPORTED) return fail(rc, "particle arrays exceed the LDS of a CU (K too large)");
+  if (rc != HYG_OK) return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  return HYG_OK;
+}
+
+int hyg_sg_run_chain_host_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, const uint16_t* meth,
+                             const uint16_t* tot, int32_t S, int32_t T, uint64_t seed, uint64_t chain_id,
+                             double* regime_probs, double* theta_out) {
+  if (!m || !pe || !regime_probs || !theta_out || (S > 0 && (!meth || !tot))) return fail(HYG_EINVAL, "null argument");
+  if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (T < 1 || S < 0) return fail(HYG_EINVAL, "no sites");
+  if (pe->n_steps_without_update < 1) return fail(HYG_EINVAL, "n_steps_without_update < 1");
+  for (int64_t i = 0; i < (int64_t)T * S; ++i)
+    if (tot[i] > m->nmax_reads) return fail(HYG_EINVAL, "total read count above the model's max_total_reads");
+  const int K = m->c.K;
+  struct Buf {
+    void* p = nullptr;
+    ~Buf() { if (p) (void)hipFree(p); }
+  } b_m, b_t, b_E, b_ws, b_p, b_st, b_th;
+  auto alloc = [](Buf& b, size_t n) { return hipMalloc(&b.p, n ? n : 1) == hipSuccess; };
+  hyg_sg_chain ch{};
+  ch.site_begin = 0;
+  ch.n_sites = T;
+  ch.seed = seed;
+  ch.chain_id = chain_id;
+  ch.out_begin = 0;
+  const size_t nc = (size_t)T * S;
+  const size_t wsb = hyg_sg_pe_workspace_bytes(m, &ch, 1, 0);
+  const int64_t rows = hyg_sgpe_theta_rows(T, pe->n_steps_without_update);
+  const size_t thb = sizeof(double) * (size_t)rows * K * K;
+  bool ok = alloc(b_m, nc * 2) && alloc(b_t, nc * 2) && alloc(b_E, sizeof(double) * T * K) && alloc(b_ws, wsb) &&
+            alloc(b_p, sizeof(double) * T * K) && alloc(b_st, 4) && alloc(b_th, thb);
+  if (!ok) return fail(HYG_ENOMEM, "device allocation failed");
+  if (nc && hipMemcpy(b_m.p, meth, nc * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (nc && hipMemcpy(b_t.p, tot, nc * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  int rc = hyg_sg_emission(m, (uint16_t*)b_m.p, (uint16_t*)b_t.p, S, T, (double*)b_E.p, nullptr);
+  if (rc) return rc;
+  rc = hyg_sg_run_chains_pe(m, pe, &ch, 1, (double*)b_E.p, b_ws.p, wsb, 0, (double*)b_p.p, (double*)b_th.p,
+                            (int32_t*)b_st.p, nullptr);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(HYG_EDEVICE, "kernel execution failed");
+  int32_t st = 0;
+  if (hipMemcpy(&st, b_st.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (hipMemcpy(regime_probs, b_p.p, sizeof(double) * T * K, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(theta_out, b_th.p, thb, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(HYG_EDEVICE, "copy failed");
+  if (st == HYG_ENOMEM) return fail(st, "pending smoothing times exceeded psi_capacity, or a sojourn outgrew the hazard rows");
   if (st != HYG_OK) return fail(st, "all particle weights became -inf");
   return HYG_OK;
 }

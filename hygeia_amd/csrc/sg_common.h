@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/hyg_sg_model.h"
+#include "../../include/hyg_sg_pe.h"
 
 namespace hyg {
 
@@ -33,8 +34,31 @@ struct SgChainDev {
   uint64_t seed;
   uint64_t chain_id;
   int32_t T;
-  int32_t pad;
+  int32_t rcap;        // parameter estimation: hazard rows per regime
+  int64_t pe_offset;   // parameter estimation: byte offset of the chain's region
+  int64_t theta_row;   // parameter estimation: first output row of theta
 };
+
+// Online parameter estimation (include/hyg_sg_pe.h), model-level inputs
+struct SgPeDev {
+  hyg_sgpe_consts c;
+  const double* theta0;        // [dim] initial theta
+  const hyg_sgpe_step* steps;  // [n] step sizes / bias corrections per update
+  const double* lgk;           // [K][lgk_stride] theta-free part of the NegBin log-pmf
+  int32_t lgk_stride;
+  int32_t pad;
+  double* theta_out;           // [rows][dim]
+};
+
+// Per-chain region of the estimation path: phi [2][256][dim], theta, ADAM
+// moments, previous / current score [dim] each, hazard rows [K][rcap], and
+// the rebuild scratch h, g, bigH[d-1], gradBigH[d-1] [K][rcap] f64 + exit [K][rcap] u8.
+__host__ __device__ inline size_t sg_pe_region_bytes(int K, int rcap) {
+  const size_t dim = (size_t)K * K;
+  const size_t b = 8 * (2 * (size_t)kSgThreads * dim + 5 * dim) + 32 * (size_t)K * rcap + 32 * (size_t)K * rcap +
+                   (size_t)K * rcap;
+  return (b + 255) / 256 * 256;
+}
 
 // Per-chain workspace: cap psi slots [K][256] f64, then the pending-time lists
 // slot[2][cap] / time[2][cap] (double-buffered), keep[cap], free[cap] (int32).
@@ -48,7 +72,8 @@ __host__ __device__ inline size_t sg_chain_ws_bytes(int K, int cap) {
 int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint16_t* meth, const uint16_t* tot,
                        int S, int64_t n_sites, double* E, void* stream);
 int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
-                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream);
-size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap);
+                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream,
+                     const SgPeDev* pe = nullptr);
+size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap, bool pe = false);
 
 }  // namespace hyg

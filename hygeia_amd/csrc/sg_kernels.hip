@@ -4,6 +4,11 @@
 //   sg_chain_kernel     SMC for the change-point model + online marginal
 //                       smoothing, one 256-thread workgroup per chain, one
 //                       particle per thread (N_max <= 256), persistent over T.
+//                       Template flag PE: with online parameter estimation
+//                       (include/hyg_sg_pe.h): the score
+//                       recursion phi, an ADAM / gradient step every `every`
+//                       steps and the rebuild of P, omega and the hazard rows
+//                       from the new theta, all inside the persistent workgroup.
 //
 // Same computations as oracle/sg_oracle.c (the arithmetic contract of
 // include/hyg_arith.h: exact fixed-point sums, hyg_exp / hyg_log, Philox), so
@@ -91,6 +96,7 @@ struct SgShared {
 struct SgLay {
   size_t st, lw, w, base, cont;  // [2][NT]: current / previous particle sets, alternating per step
   size_t anc, lwres, logq, sidx, cum, xk, xi, BK, logP, red, lsev, scr, meanb, okb, logm, logQ, psil, sh, total;
+  size_t pm, gfr, gct, pei;  // parameter estimation: model, per-particle gradient entries [2][NT], ints
   int nl;  // psi slots resident in LDS (slot ids 0 .. nl-1; the rest live in the workspace)
 };
 
@@ -100,7 +106,7 @@ __host__ __device__ inline size_t sg_align(size_t x) { return (x + 15) / 16 * 16
 // waves join the block reductions, sorts (on dummy keys) and the smoothing tasks)
 __host__ __device__ inline int sg_block_threads(int K) { return K <= 8 ? 512 : 256; }
 
-__host__ __device__ inline SgLay sg_layout(int K, int cap) {
+__host__ __device__ inline SgLay sg_layout(int K, int cap, bool pe) {
   SgLay l{};
   const int NT = kSgThreads, NB = sg_block_threads(K), NW = NB / 64;
   size_t o = 0;
@@ -126,6 +132,12 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap) {
   l.logm = o; o = sg_align(o + 8 * (NT + 1));
   l.logQ = o; o = sg_align(o + 8 * (NT + 1));
   l.sh = o; o = sg_align(o + sizeof(SgShared));
+  if (pe) {
+    l.pm = o; o = sg_align(o + sizeof(hyg_sgpe_model));
+    l.gfr = o; o = sg_align(o + 8 * 2 * NT);
+    l.gct = o; o = sg_align(o + 8 * 2 * NT);
+    l.pei = o; o = sg_align(o + 4 * (2 * HYG_KMAX + 8));
+  }
   const size_t slot = 8 * (size_t)K * NT;
   const size_t budget = 160 * 1024 - 2048;  // headroom below the 160 KiB of a CU (launches at 163808 B fail)
   int nl = o < budget ? (int)((budget - o) / slot) : 0;
@@ -137,7 +149,7 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap) {
   return l;
 }
 
-size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap) { return sg_layout(c.K, psi_cap).total; }
+size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap, bool pe) { return sg_layout(c.K, psi_cap, pe).total; }
 
 // ------------------------------------------------------------- emission
 // E[t][r] = sum_s log BB(y_ts | n_ts, alpha_r, beta_r) in the oracle's term
@@ -174,6 +186,92 @@ sg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
   }
 }
 
+
+// ------------------------------------------- parameter estimation helpers
+// The chain's region of the workspace (sg_pe_region_bytes).
+struct SgPeChain {
+  double* phi;  // [2][NT][dim] score recursion, particle-major
+  double *th, *am, *av, *gp, *gc;
+  hyg_sgpe_row* rows;            // [K][rcap]
+  double *h, *g, *Hm1, *gm1;     // rebuild scratch [K][rcap]
+  uint8_t* ex;                   // [K][rcap]
+  int rcap;
+};
+__device__ __forceinline__ SgPeChain sg_pe_chain(uint8_t* ws, const SgChainDev& ch, int K) {
+  SgPeChain c;
+  const size_t dim = (size_t)K * K, kr = (size_t)K * ch.rcap;
+  c.phi = (double*)(ws + ch.pe_offset);
+  c.th = c.phi + 2 * (size_t)kSgThreads * dim;
+  c.am = c.th + dim;
+  c.av = c.am + dim;
+  c.gp = c.av + dim;
+  c.gc = c.gp + dim;
+  c.rows = (hyg_sgpe_row*)(c.gc + dim);
+  c.h = (double*)(c.rows + kr);
+  c.g = c.h + kr;
+  c.Hm1 = c.g + kr;
+  c.gm1 = c.Hm1 + kr;
+  c.ex = (uint8_t*)(c.gm1 + kr);
+  c.rcap = ch.rcap;
+  return c;
+}
+
+// setUnknownParameters (singleGroup.h:197-270) for the chain's current theta:
+// P / log P / omega into LDS, then the hazard rows 0 .. L-1 of every regime
+// (include/hyg_sg_pe.h): the NegBin terms in parallel over (r, d), the
+// sequential bigH / gradBigH recursion one lane per regime, the finished rows
+// in parallel. Called by every thread; ends on a barrier.
+template <int NB>
+__device__ void sg_pe_rebuild(const SgPeDev& pe, const hyg_sg_consts& c, const SgPeChain& pc, hyg_sgpe_model* pm,
+                              int* Lr, int* exr, int K, int u, int L) {
+  const int tid = threadIdx.x;
+  if (L > pc.rcap) L = pc.rcap;
+  if (tid < K) hyg_sgpe_set_regime(pc.th, K, tid, pm);
+  __syncthreads();
+  for (int i = tid; i < K * L; i += NB) {
+    const int r = i / L, d = i - r * L;
+    double h, g;
+    hyg_sgpe_hazard_point(pm, r, d, u, c.kappa[r], pe.lgk + (size_t)r * pe.lgk_stride, &h, &g);
+    const size_t o = (size_t)r * pc.rcap + d;
+    pc.h[o] = h;
+    pc.g[o] = g;
+  }
+  __syncthreads();
+  if (tid < K) {
+    const size_t o = (size_t)tid * pc.rcap;
+    const int l = hyg_sgpe_hazard_scan(pc.h + o, pc.g + o, u, L, pc.Hm1 + o, pc.gm1 + o, pc.ex + o);
+    Lr[tid] = l;
+    exr[tid] = pc.ex[o + l - 1];
+  }
+  __syncthreads();
+  for (int i = tid; i < K * L; i += NB) {
+    const int r = i / L, d = i - r * L;
+    if (d < Lr[r]) {
+      const size_t o = (size_t)r * pc.rcap + d;
+      pc.rows[o] = hyg_sgpe_hazard_row(pc.h[o], pc.g[o], pc.Hm1[o], pc.gm1[o], pc.ex[o], d, u);
+    }
+  }
+  __syncthreads();
+}
+
+// sg_trans_parts of the estimation path plus the particle's gradient entries:
+// gomg = d log rho / d theta_omega (fresh particles from it), gcont = the
+// continuation's entry. `over` is set when a sojourn outruns the rows of a
+// regime whose hazard has not exited.
+__device__ __forceinline__ void sg_pe_parts(const SgPeChain& pc, const int* Lr, const int* exr, int u, uint32_t s,
+                                            double& base, double& cont, double& gomg, double& gcont, int& over) {
+  const int d = sg_d(s), r = sg_r(s);
+  int di = d - 1;
+  if (di >= Lr[r]) {
+    if (!exr[r]) over = 1;
+    di = Lr[r] - 1;
+  }
+  const hyg_sgpe_row w = pc.rows[(size_t)r * pc.rcap + di];
+  base = (d >= u) ? w.base : HYG_NINF;
+  cont = w.cont;
+  gomg = w.gomg;
+  gcont = w.gcont;
+}
 
 // --------------------------------------------------------- chain kernel
 // order key of a double: ascending key == ascending value (-0.0 == +0.0)
@@ -232,11 +330,11 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
 // and backward kernels, and the smoothing split into (pending time, regime)
 // tasks over all waves with the psi rows resident in LDS (up to 32 slots,
 // the rest in the chain's workspace region).
-template <int KT, int NB>
+template <int KT, int NB, bool PE>
 __global__ void __launch_bounds__(NB)
 sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const double* __restrict__ E,
                 uint8_t* __restrict__ ws, int cap, double* __restrict__ probs, int32_t* __restrict__ status_out,
-                SgLay lay, unsigned long long* __restrict__ dbg) {
+                SgLay lay, unsigned long long* __restrict__ dbg, SgPeDev pe) {
   constexpr int NT = kSgThreads, NW = NB / 64, K = KT;  // NT: particle slots, NB: threads
   const hyg_sg_consts& c = *md.consts;
   const int Nmax = c.Nmax, u = c.u, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
@@ -257,7 +355,8 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   uint64_t* xk = (uint64_t*)(smem + lay.xk);
   int* xi = (int*)(smem + lay.xi);
   double* BK = (double*)(smem + lay.BK);
-  double* logP = (double*)(smem + lay.logP);
+  hyg_sgpe_model* pm = PE ? (hyg_sgpe_model*)(smem + lay.pm) : nullptr;
+  double* logP = PE ? pm->logP : (double*)(smem + lay.logP);
   unsigned char* red = smem + lay.red;
   double* lsev = (double*)(smem + lay.lsev);
   double* scr = (double*)(smem + lay.scr) + wv * NT;
@@ -280,7 +379,30 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   };
 
   for (int i = tid; i < cap; i += NB) freel[i] = cap - 1 - i;
-  for (int i = tid; i < K * K; i += NB) logP[i] = c.logP[i];
+  if (!PE)
+    for (int i = tid; i < K * K; i += NB) logP[i] = c.logP[i];
+  // parameter estimation state (OnlineParameterEstimation.h:42-176)
+  double* gfr = PE ? (double*)(smem + lay.gfr) : nullptr;  // [2][NT] gomg of each particle
+  double* gct = PE ? (double*)(smem + lay.gct) : nullptr;  // [2][NT] continuation entry
+  int* peLr = PE ? (int*)(smem + lay.pei) : nullptr;       // [KMAX] rows valid per regime
+  int* peEx = PE ? peLr + HYG_KMAX : nullptr;              // [KMAX] exited at the last row
+  SgPeChain pc{};
+  constexpr int dim = K * K, jw = K * (K - 1);
+  const int every = PE ? pe.c.every : 1;
+  if constexpr (PE) {
+    pc = sg_pe_chain(ws, ch, K);
+    for (int j = tid; j < dim; j += NB) {
+      const double th0 = pe.theta0[j];
+      pc.th[j] = th0;
+      pc.am[j] = 0.0;
+      pc.av[j] = 0.0;
+      pc.gp[j] = 0.0;  // gradientCurr at t = 0: the filtered mean of phi = 0
+      pe.theta_out[(size_t)ch.theta_row * dim + j] = th0;
+    }
+    for (int i = tid; i < K * dim; i += NB) pc.phi[i] = 0.0;  // phi of the K initial particles
+    __syncthreads();
+    sg_pe_rebuild<NB>(pe, c, pc, pm, peLr, peEx, K, u, 1 + every + 1);
+  }
   for (int i = tid; i <= NT; i += NB) logm[i] = hyg_log((double)i);  // log(M - k) of the K loop
   // phase timers: 0 copy, 1 sort, 2 K loop, 3 residual / keep-top, 4 weights,
   // 5 normalise, 6 smoothing, 7 compaction; counters 8 optimal steps, 9
@@ -306,7 +428,17 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   uint32_t my_st = sg_pack(1, tid < K ? tid : 0);
   double my_lw = (tid < K) ? -c.log_K + Ech[tid] : HYG_NINF;
   double my_base = HYG_NINF, my_cont = HYG_NINF;
-  if (tid < K) sg_trans_parts(md, u, my_st, my_base, my_cont);
+  if constexpr (PE) {
+    if (tid < K) {
+      double gf, gcn;
+      int ov = 0;
+      sg_pe_parts(pc, peLr, peEx, u, my_st, my_base, my_cont, gf, gcn, ov);
+      gfr[tid] = gf;
+      gct[tid] = gcn;
+    }
+  } else {
+    if (tid < K) sg_trans_parts(md, u, my_st, my_base, my_cont);
+  }
   double mx0;
   int fin;
   block_max_cnt<NB>(my_lw, (tid < K && hyg_isfinite(my_lw)) ? 1 : 0, red, &mx0, &fin);
@@ -581,9 +713,90 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         st_[cb * NT + tid] = my_st;
         lw_[cb * NT + tid] = my_lw;
         w_[cb * NT + tid] = my_w;
-        sg_trans_parts(md, u, my_st, my_base, my_cont);  // consumed next step
+        if (!PE) sg_trans_parts(md, u, my_st, my_base, my_cont);  // consumed next step
       }
       SG_PH(5);
+      if constexpr (PE) {
+        // updatePhi (OnlineParameterEstimation.h:118-150) with the gradients of
+        // the log transition density (singleGroup.h:641-717) under the current
+        // theta, in the oracle's order (oracle/sg_oracle.c)
+        const double* phiP = pc.phi + (size_t)pb * NT * dim;
+        double* phiC = pc.phi + (size_t)cb * NT * dim;
+        const double* gfrP = gfr + pb * NT;
+        const uint32_t* stPP = st_ + pb * NT;
+        if (tid < M) {  // continuing particle: phi of the ancestor + the omega entry
+          const int a = anc[tid];
+          const int jr = jw + sg_r(my_st);
+          const double gcv = gct[pb * NT + a];
+          const double* src = phiP + (size_t)a * dim;
+          double* dst = phiC + (size_t)tid * dim;
+#pragma unroll 4
+          for (int j = 0; j < dim; ++j) dst[j] = src[j] + ((j == jr) ? gcv : 0.0);
+        }
+        for (int pq = tid; pq < K * dim; pq += NB) {  // fresh particle (1, q), coordinate j
+          const int q = pq / dim, j = pq - q * dim;
+          const int rb = (j < jw) ? j / (K - 1) : -1;
+          double acc = 0.0;
+          for (int n = 0; n < Np; ++n) {
+            const uint32_t sn = stPP[n];
+            const int rp = sg_r(sn);
+            double g = 0.0;
+            if (q != rp && sg_d(sn) >= u) {
+              if (j == jw + rp) {
+                g = gfrP[n];
+              } else if (rb == rp) {
+                const int i = j - rp * (K - 1), jj = (i < rp) ? i : i + 1;
+                g = -pm->P[rp * K + jj];
+                if (jj == q) g = g + 1.0;
+              }
+            }
+            acc = acc + BK[q * NT + n] * (phiP[(size_t)n * dim + j] + g);
+          }
+          phiC[(size_t)(M + q) * dim + j] = acc;
+        }
+        __syncthreads();
+        if (t % every == 0) {
+          // updateGradients (:151-156): filtered mean of phi, difference to the
+          // previous one; GradientAscent::iterate (GradientAscent.h:82-105)
+          const double* wCur = w_ + cb * NT;
+          for (int j = tid; j < dim; j += NB) {
+            double est = 0.0;
+            for (int n = 0; n < N; ++n) est = est + wCur[n] * phiC[(size_t)n * dim + j];
+            pc.gc[j] = est - pc.gp[j];
+            pc.gp[j] = est;
+          }
+          __syncthreads();
+          double l1 = 0.0;
+          if (pe.c.normalise && !pe.c.use_adam)
+            for (int j = 0; j < dim; ++j) l1 = l1 + fabs(pc.gc[j]);
+          const int it = t / every - 1;
+          const double lr = pe.steps[it].lr, c1 = pe.steps[it].c1, c2 = pe.steps[it].c2;
+          for (int j = tid; j < dim; j += NB) {
+            double am = pc.am[j], av = pc.av[j];
+            const double th = hyg_sgpe_update(pe.c.use_adam, pe.c.normalise, pe.c.beta1, pe.c.beta2, pe.c.eps, lr,
+                                              c1, c2, pc.th[j], pc.gc[j], l1, &am, &av);
+            pc.th[j] = th;
+            pc.am[j] = am;
+            pc.av[j] = av;
+            pe.theta_out[(size_t)(ch.theta_row + t / every) * dim + j] = th;
+          }
+          // rows for every sojourn the set can reach before the next rebuild
+          const int maxd = (int)block_max<NB>((tid < N) ? (double)sg_d(my_st) : 0.0, red);
+          __syncthreads();
+          sg_pe_rebuild<NB>(pe, c, pc, pm, peLr, peEx, K, u, maxd + every + 1);
+        }
+        int ov = 0;
+        if (tid < N) {
+          double gf, gcn;
+          sg_pe_parts(pc, peLr, peEx, u, my_st, my_base, my_cont, gf, gcn, ov);
+          gfr[cb * NT + tid] = gf;
+          gct[cb * NT + tid] = gcn;
+        }
+        if (__syncthreads_or(ov)) {
+          status = HYG_ENOMEM;
+          break;
+        }
+      }
     }
     // ---- online marginal smoothing: updatePsi (OnlineMarginalSmoothing.h:152-197)
     //      of the pending times, initialisePsi (:132-150) of time t, storeEstimates
@@ -766,15 +979,15 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
 }
 
 // ------------------------------------------------------------- launches
-template <int KT, int NB>
+template <int KT, int NB, bool PE>
 static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, int n_chains, const double* E,
                             uint8_t* ws, int cap, double* probs, int32_t* status, const SgLay& lay,
-                            unsigned long long* dbg, hipStream_t s, hipError_t* err) {
-  *err = hipFuncSetAttribute((const void*)sg_chain_kernel<KT, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            unsigned long long* dbg, hipStream_t s, const SgPeDev& pe, hipError_t* err) {
+  *err = hipFuncSetAttribute((const void*)sg_chain_kernel<KT, NB, PE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lay.total);
   if (*err != hipSuccess) return;
-  hipLaunchKernelGGL((sg_chain_kernel<KT, NB>), dim3(n_chains), dim3(NB), lay.total, s, md, chains_dev, E, ws,
-                     cap, probs, status, lay, dbg);
+  hipLaunchKernelGGL((sg_chain_kernel<KT, NB, PE>), dim3(n_chains), dim3(NB), lay.total, s, md, chains_dev, E, ws,
+                     cap, probs, status, lay, dbg, pe);
   *err = hipGetLastError();
 }
 // ------------------------------------------------------------- launches
@@ -790,10 +1003,13 @@ int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint1
 
 
 int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
-                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream) {
+                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream,
+                     const SgPeDev* pe) {
   if (n_chains <= 0) return HYG_OK;
   if (c.Nmax > kSgThreads || c.K < 2 || c.K > HYG_KMAX) return HYG_EUNSUPPORTED;
-  const SgLay lay = sg_layout(c.K, psi_cap);
+  const SgLay lay = sg_layout(c.K, psi_cap, pe != nullptr);
+  SgPeDev ped{};
+  if (pe) ped = *pe;
   if (lay.total > 160 * 1024) return HYG_EUNSUPPORTED;
   static const bool want_dbg = getenv("HYG_SG_PHASES") != nullptr;
   unsigned long long* dbg = nullptr;
@@ -802,8 +1018,15 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
   if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * 16 * n_chains, s);
   hipError_t err = hipErrorInvalidValue;
   switch (c.K) {
-#define SG_CASE(k) \
-  case k: launch_chain_kt<k, (k <= 8 ? 512 : 256)>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, dbg, s, &err); break;
+#define SG_CASE(k)                                                                                               \
+  case k:                                                                                                        \
+    if (pe)                                                                                                      \
+      launch_chain_kt<k, (k <= 8 ? 512 : 256), true>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, \
+                                                     dbg, s, ped, &err);                                         \
+    else                                                                                                         \
+      launch_chain_kt<k, (k <= 8 ? 512 : 256), false>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status,     \
+                                                      lay, dbg, s, ped, &err);                                   \
+    break;
     SG_CASE(2) SG_CASE(3) SG_CASE(4) SG_CASE(5) SG_CASE(6) SG_CASE(7) SG_CASE(8) SG_CASE(9)
     SG_CASE(10) SG_CASE(11) SG_CASE(12) SG_CASE(13) SG_CASE(14) SG_CASE(15) SG_CASE(16)
 #undef SG_CASE

@@ -164,8 +164,8 @@ int hyg_tg_last_kernel_ms(float* ms3);
  *       epsilon, useOnlineParameterEstimation = false, ...)
  *     -> regimeProbabilityEstimates [T][1 + K] (position, P(r = 1..K))
  *   (singleGroup.cpp:76-189; called by bin/estimate_parameters_and_regimes:303-322).
- * Online parameter estimation (useOnlineParameterEstimation) is not part of
- * this path. */
+ * Online parameter estimation (useOnlineParameterEstimation = TRUE, the
+ * pipeline's --estimate_parameters) is the hyg_sg_*_pe family below. */
 typedef struct hyg_sg_params {
   int32_t n_regimes;          /* K = vartheta[1] (model_functions.R:36-59)          */
   int32_t minimum_duration;   /* u = vartheta[0]                                    */
@@ -218,6 +218,47 @@ int hyg_sg_run_chains(const hyg_sg_model* model, const hyg_sg_chain* chains, int
 int hyg_sg_run_chain_host(const hyg_sg_model* model, const uint16_t* meth, const uint16_t* tot,
                           int32_t n_samples, int32_t n_sites, uint64_t seed, uint64_t chain_id,
                           double* regime_probs);
+
+/* ---- online parameter estimation
+ * runOnlineCombinedInferenceCpp(..., useOnlineParameterEstimation = TRUE,
+ *     normaliseGradients, useAdam, nStepsWithoutParameterUpdate,
+ *     learningRateExponent, learningRateFactor, ...) -> thetaEstimates
+ * (singleGroup.cpp:76-189, OnlineCombinedInference.h:48-118,
+ * OnlineParameterEstimation.h:42-176, GradientAscent.h:62-155), run by the
+ * two-group pipeline's `hygeia estimate_parameters_and_regimes ...
+ * --estimate_regime_probabilities --estimate_parameters`
+ * (modules/two_group/2_estimate_parameters_and_regimes.nf:38-52). The
+ * regime probabilities are smoothed under the moving theta, as the reference.
+ * Requires is_kappa_fixed (the pipeline default); else HYG_EUNSUPPORTED. */
+typedef struct hyg_sg_pe_params {
+  int32_t use_adam;               /* --use_adam, TRUE                          */
+  int32_t normalise_gradients;    /* --normalise_gradients, FALSE              */
+  int32_t n_steps_without_update; /* --n_steps_without_parameter_update, 200   */
+  int32_t _pad;
+  double learning_rate_exponent;  /* --learning_rate_exponent, 0.1             */
+  double learning_rate_factor;    /* --learning_rate_factor, 0.01              */
+} hyg_sg_pe_params;
+
+void hyg_sg_pe_params_default(hyg_sg_pe_params* pe);
+/* Rows of theta the chains report: per chain 1 + (n_sites - 1) / every (the
+ * initial theta, then theta after each update at t = every, 2 every, ...);
+ * chain i's rows follow chain i-1's. The reference's thetaEstimates row t
+ * (t = 0 .. T-1) is row t / every of its chain. */
+int64_t hyg_sg_pe_theta_rows(const hyg_sg_chain* chains, int32_t n_chains, int32_t every);
+size_t hyg_sg_pe_workspace_bytes(const hyg_sg_model* model, const hyg_sg_chain* chains, int32_t n_chains,
+                                 int32_t psi_capacity);
+/* As hyg_sg_run_chains, with theta updated online; theta_out [rows][K^2] f64
+ * (device). status may also be HYG_ENOMEM when a sojourn outgrows the
+ * hazard table (HYG_SGPE_DCAP rows) before the hazard's exit. */
+int hyg_sg_run_chains_pe(const hyg_sg_model* model, const hyg_sg_pe_params* pe, const hyg_sg_chain* chains,
+                         int32_t n_chains, const double* emission, void* workspace, size_t workspace_bytes,
+                         int32_t psi_capacity, double* regime_probs, double* theta_out, int32_t* status,
+                         void* stream);
+/* Host-pointer convenience for one chain: regime_probs [T][K], theta_out
+ * [1 + (T - 1) / every][K^2]. */
+int hyg_sg_run_chain_host_pe(const hyg_sg_model* model, const hyg_sg_pe_params* pe, const uint16_t* meth,
+                             const uint16_t* tot, int32_t n_samples, int32_t n_sites, uint64_t seed,
+                             uint64_t chain_id, double* regime_probs, double* theta_out);
 
 /* ================================================ aggregation and DMPs
  * The consumers of the two-group trajectories:

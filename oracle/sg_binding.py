@@ -32,6 +32,26 @@ class SgParams(C.Structure):
     ]
 
 
+class SgPeParams(C.Structure):
+    """Mirror of hyg_sg_pe_params (include/hygeia_amd.h); defaults are the
+    estimate_parameters_and_regimes flags (bin/estimate_parameters_and_regimes:130-200)."""
+
+    _fields_ = [("use_adam", C.c_int32), ("normalise_gradients", C.c_int32),
+                ("n_steps_without_update", C.c_int32), ("_pad", C.c_int32),
+                ("learning_rate_exponent", C.c_double), ("learning_rate_factor", C.c_double)]
+
+
+def make_pe(use_adam=True, normalise_gradients=False, every=200, lr_exponent=0.1, lr_factor=0.01):
+    pe = SgPeParams()
+    pe.use_adam, pe.normalise_gradients, pe.n_steps_without_update = int(use_adam), int(normalise_gradients), every
+    pe.learning_rate_exponent, pe.learning_rate_factor = lr_exponent, lr_factor
+    return pe
+
+
+class SgPeRow(C.Structure):
+    _fields_ = [("base", C.c_double), ("cont", C.c_double), ("gomg", C.c_double), ("gcont", C.c_double)]
+
+
 class SgConsts(C.Structure):
     _fields_ = [
         ("K", C.c_int32), ("u", C.c_int32), ("Nmax", C.c_int32), ("is_kappa_fixed", C.c_int32),
@@ -92,6 +112,10 @@ def lib():
         vp, i32, u64 = C.c_void_p, C.c_int32, C.c_uint64
         L.oracle_sg_chain.restype = i32
         L.oracle_sg_chain.argtypes = [C.POINTER(SgParams), vp, i32, u64, u64, vp, vp]
+        L.oracle_sg_chain_pe.restype = i32
+        L.oracle_sg_chain_pe.argtypes = [C.POINTER(SgParams), C.POINTER(SgPeParams), vp, i32, u64, u64, vp, vp]
+        L.oracle_sg_pe_hazard.restype = i32
+        L.oracle_sg_pe_hazard.argtypes = [C.POINTER(SgParams), vp, i32, vp, vp]
         L.oracle_sg_emission.restype = i32
         L.oracle_sg_emission.argtypes = [C.POINTER(SgParams), vp, vp, i32, C.c_int64, vp]
         L.oracle_sg_hazard.restype = i32
@@ -150,3 +174,26 @@ def hazard(p, r, n):
     if rc != 0:
         raise ValueError(rc)
     return out, ex, dcap.value
+
+
+def chain_pe(p, pe, E, seed=0, chain_id=0):
+    """SMC + online smoothing with online parameter estimation: regime
+    probabilities [T][K] and theta rows [1 + (T-1)//every][K^2]."""
+    E = np.ascontiguousarray(E, np.float64)
+    T, K = E.shape[0], p.n_regimes
+    probs = np.empty((T, K), np.float64)
+    theta = np.full((1 + (T - 1) // pe.n_steps_without_update, K * K), np.nan)
+    rc = lib().oracle_sg_chain_pe(C.byref(p), C.byref(pe), _ptr(E), T, seed, chain_id, _ptr(probs), _ptr(theta))
+    return {"status": rc, "regime_probs": probs, "theta": theta}
+
+
+def pe_hazard(p, theta, L):
+    """hazard rows of the estimation path: (base, cont, gomg, gcont) [K][L] and rows valid per regime"""
+    K = p.n_regimes
+    rows = np.zeros((K, L, 4), np.float64)
+    Lr = np.zeros(K, np.int32)
+    th = np.ascontiguousarray(theta, np.float64)
+    rc = lib().oracle_sg_pe_hazard(C.byref(p), _ptr(th), L, _ptr(rows), _ptr(Lr))
+    if rc != 0:
+        raise ValueError(rc)
+    return rows, Lr

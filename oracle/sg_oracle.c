@@ -19,6 +19,14 @@
  * (R RNG, sequential double sums, not buildable here: RcppArmadillo absent)
  * the results are "parity unpinned"; tests/test_sg_oracle.py pins the model
  * tables and the statistical behaviour. Only used by tests/ and bench.py.
+ *
+ * Online parameter estimation (oracle_sg_chain_pe): the phi
+ * recursion of OnlineParameterEstimation.h:118-150 (continuing particle n:
+ * phi_anc + grad; fresh particle (1, q): sum_n K_q(n) (phi_n + grad_qn) in n
+ * order), the filtered score sum_n W_n phi_n (Smc.h:341-350) every
+ * `every` steps, the ADAM / gradient step (GradientAscent.h:82-155) and the
+ * rebuild of P, omega and the hazard tables from the new theta
+ * (include/hyg_sg_pe.h, shared with the kernel).
  */
 #include <math.h>
 #include <stdint.h>
@@ -27,6 +35,7 @@
 
 #include "../include/hyg_arith.h"
 #include "../include/hyg_sg_model.h"
+#include "../include/hyg_sg_pe.h"
 
 #define HYG_RNG_SG_SYSTEMATIC 5
 
@@ -35,9 +44,45 @@ typedef struct {
   int dcap;
   double* hz;
   uint8_t* ex;
+  /* online parameter estimation: theta-dependent model and hazard rows */
+  int pe;
+  hyg_sgpe_consts pc;
+  hyg_sgpe_model pm;
+  int rcap;              /* rows per regime: min(T + 1, HYG_SGPE_DCAP) */
+  int Lr[HYG_KMAX], exited[HYG_KMAX];
+  int overflow;          /* a lookup beyond the rows of a regime that has not exited */
+  hyg_sgpe_row* rows;    /* [K][rcap] */
+  double *lgk, *h, *g, *Hm1s, *gm1s; /* lgk [K][rcap], scratch [rcap] */
+  uint8_t* exs;
 } sg_model;
 
+/* rebuild of the theta-dependent model (setUnknownParameters, singleGroup.h:197-270,
+ * extendAuxiliaryQuantities :271-335) with L rows per regime */
+static void sgm_pe_rebuild(sg_model* m, const double* theta, int L) {
+  const int K = m->c.K, u = m->c.u;
+  if (L > m->rcap) L = m->rcap;
+  for (int r = 0; r < K; ++r) hyg_sgpe_set_regime(theta, K, r, &m->pm);
+  for (int r = 0; r < K; ++r) {
+    const double* lgk = m->lgk + (size_t)r * m->rcap;
+    for (int d = 0; d < L; ++d) hyg_sgpe_hazard_point(&m->pm, r, d, u, m->pc.kappa[r], lgk, &m->h[d], &m->g[d]);
+    const int Lr = hyg_sgpe_hazard_scan(m->h, m->g, u, L, m->Hm1s, m->gm1s, m->exs);
+    m->Lr[r] = Lr;
+    m->exited[r] = m->exs[Lr - 1];
+    for (int d = 0; d < Lr; ++d)
+      m->rows[(size_t)r * m->rcap + d] = hyg_sgpe_hazard_row(m->h[d], m->g[d], m->Hm1s[d], m->gm1s[d], m->exs[d], d, u);
+  }
+}
+static const hyg_sgpe_row* sgm_pe_row(sg_model* m, int dp, int r) {
+  int d = dp - 1;
+  if (d >= m->Lr[r]) {
+    if (!m->exited[r]) m->overflow = 1;
+    d = m->Lr[r] - 1;
+  }
+  return m->rows + (size_t)r * m->rcap + d;
+}
+
 static int sgm_init(sg_model* m, const hyg_sg_params* p, int max_duration) {
+  memset(m, 0, sizeof(*m));
   int rc = hyg_sg_derive(p, &m->c);
   if (rc) return rc;
   m->dcap = hyg_sg_hazard_len(&m->c, max_duration);
@@ -47,12 +92,21 @@ static int sgm_init(sg_model* m, const hyg_sg_params* p, int max_duration) {
   hyg_sg_hazard_fill(&m->c, m->dcap, m->hz, m->ex);
   return HYG_OK;
 }
-static void sgm_free(sg_model* m) { free(m->hz); free(m->ex); }
+static void sgm_free(sg_model* m) {
+  free(m->hz); free(m->ex);
+  if (m->pe) { free(m->rows); free(m->lgk); free(m->h); free(m->g); free(m->Hm1s); free(m->gm1s); free(m->exs); }
+}
 
 /* Model::evaluateLogTransitionDensity (singleGroup.h:569-608) for the two
  * cases the change-point SMC evaluates: (1, r') from (d, r) and (d+1, r) from (d, r). */
-static double sg_trans(const sg_model* m, int dc, int rc, int dp, int rp) {
+static double sg_trans(sg_model* m, int dc, int rc, int dp, int rp) {
   const int K = m->c.K;
+  if (m->pe) {
+    const hyg_sgpe_row* w = sgm_pe_row(m, dp, rp);
+    if (dc == 1 && rc != rp && dp >= m->c.u) return w->base + m->pm.logP[rp * K + rc];
+    if (dc > 1 && rc == rp) return w->cont;
+    return -INFINITY;
+  }
   int d = dp - 1;
   if (d >= m->dcap) d = m->dcap - 1;
   const double* h = m->hz + ((size_t)rp * m->dcap + d) * 2;
@@ -138,14 +192,52 @@ int64_t oracle_sg_optimal_steps = 0; /* capped steps resampled by the optimal sc
 
 /* One chain over T sites: E [T][K] emission table. Writes probs [T][K]
  * (the smoothed regime probabilities). Returns HYG_OK / HYG_ENUMERIC / HYG_ENOMEM. */
-int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t seed, uint64_t chain_id,
-                    double* probs, int32_t* nparts_out) {
+static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, const double* E, int T, uint64_t seed,
+                         uint64_t chain_id, double* probs, int32_t* nparts_out, double* theta_out) {
   if (T < 1 || T >= HYG_DMAX - 2) return HYG_EINVAL;
   sg_model mo;
   int rc = sgm_init(&mo, p, T + 1);
   if (rc) return rc;
   const hyg_sg_consts* c = &mo.c;
   const int K = c->K, Nmax = c->Nmax;
+  /* online parameter estimation state (OnlineParameterEstimation.h:42-176) */
+  double *theta = NULL, *am = NULL, *av = NULL, *gprev = NULL, *gcur = NULL, *phiP = NULL, *phiC = NULL;
+  hyg_sgpe_step* steps = NULL;
+  int dim = 0, every = 1, iter = 0;
+  if (pe) {
+    rc = hyg_sgpe_consts_make(p, pe, &mo.pc);
+    if (rc) { sgm_free(&mo); return rc; }
+    mo.pe = 1;
+    dim = mo.pc.dim;
+    every = mo.pc.every;
+    mo.rcap = (T + 1 < HYG_SGPE_DCAP) ? T + 1 : HYG_SGPE_DCAP;
+    const int nst = (int)hyg_sgpe_theta_rows(T, every);
+    mo.rows = malloc(sizeof(hyg_sgpe_row) * (size_t)K * mo.rcap);
+    mo.lgk = malloc(sizeof(double) * (size_t)K * mo.rcap);
+    mo.h = malloc(sizeof(double) * mo.rcap);
+    mo.g = malloc(sizeof(double) * mo.rcap);
+    mo.Hm1s = malloc(sizeof(double) * mo.rcap);
+    mo.gm1s = malloc(sizeof(double) * mo.rcap);
+    mo.exs = malloc(mo.rcap);
+    theta = malloc(sizeof(double) * dim);
+    am = calloc(dim, sizeof(double));
+    av = calloc(dim, sizeof(double));
+    gprev = calloc(dim, sizeof(double));
+    gcur = calloc(dim, sizeof(double));
+    phiP = calloc((size_t)Nmax * dim, sizeof(double));
+    phiC = calloc((size_t)Nmax * dim, sizeof(double));
+    steps = malloc(sizeof(hyg_sgpe_step) * (nst + 1));
+    if (!mo.rows || !mo.lgk || !mo.h || !mo.g || !mo.Hm1s || !mo.gm1s || !mo.exs || !theta || !am || !av ||
+        !gprev || !gcur || !phiP || !phiC || !steps) {
+      rc = HYG_ENOMEM;
+      goto pe_fail;
+    }
+    hyg_sgpe_steps_fill(pe, nst + 1, steps);
+    hyg_sgpe_lgk_fill(mo.pc.kappa, K, mo.rcap, mo.lgk);
+    memcpy(theta, p->theta, sizeof(double) * dim);
+    sgm_pe_rebuild(&mo, theta, 1 + every + 1);
+    if (theta_out) memcpy(theta_out, theta, sizeof(double) * dim);
+  }
   int *dP = malloc(sizeof(int) * Nmax), *rP = malloc(sizeof(int) * Nmax), *dC = malloc(sizeof(int) * Nmax),
       *rC = malloc(sizeof(int) * Nmax), *anc = malloc(sizeof(int) * Nmax), *idx = malloc(sizeof(int) * Nmax);
   double *lwP = malloc(sizeof(double) * Nmax), *lwC = malloc(sizeof(double) * Nmax),
@@ -313,6 +405,60 @@ int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t see
       if (!(logZ > -INFINITY)) { rc = HYG_ENUMERIC; goto done; }
       for (int n = 0; n < N; ++n) wC[n] = hyg_exp(lwC[n] - logZ);
       if (nparts_out) nparts_out[t] = N;
+      if (mo.pe) {
+        /* updatePhi (OnlineParameterEstimation.h:118-150): phiCurr from phiPrev
+         * (gradients of the log transition density, singleGroup.h:641-717) */
+        const int jw = K * (K - 1);
+        for (int n = 0; n < M; ++n) {
+          const int a = anc[n];
+          const hyg_sgpe_row* w = sgm_pe_row(&mo, dP[a], rP[a]);
+          for (int j = 0; j < dim; ++j)
+            phiC[(size_t)n * dim + j] = phiP[(size_t)a * dim + j] + ((j == jw + rC[n]) ? w->gcont : 0.0);
+        }
+        for (int q = 0; q < K; ++q) {
+          for (int j = 0; j < dim; ++j) {
+            double acc = 0.0;
+            for (int n = 0; n < Np; ++n) {
+              const int rp = rP[n];
+              double g = 0.0;
+              if (q != rp && dP[n] >= c->u) {
+                if (j == jw + rp) {
+                  g = sgm_pe_row(&mo, dP[n], rp)->gomg;
+                } else if (j >= rp * (K - 1) && j < (rp + 1) * (K - 1)) {
+                  const int i = j - rp * (K - 1), jj = (i < rp) ? i : i + 1;
+                  g = -mo.pm.P[rp * K + jj];
+                  if (jj == q) g = g + 1.0;
+                }
+              }
+              acc = acc + BK[q * Nmax + n] * (phiP[(size_t)n * dim + j] + g);
+            }
+            phiC[(size_t)(M + q) * dim + j] = acc;
+          }
+        }
+        if (t % every == 0) {
+          /* updateGradients (:151-156) + GradientAscent::iterate (GradientAscent.h:82-105) */
+          double l1 = 0.0;
+          for (int j = 0; j < dim; ++j) {
+            double est = 0.0;
+            for (int n = 0; n < N; ++n) est = est + wC[n] * phiC[(size_t)n * dim + j];
+            gcur[j] = est - gprev[j];
+            gprev[j] = est;
+            l1 = l1 + fabs(gcur[j]);
+          }
+          for (int j = 0; j < dim; ++j) theta[j] = hyg_sgpe_update(mo.pc.use_adam, mo.pc.normalise, mo.pc.beta1, mo.pc.beta2, mo.pc.eps,
+                                       steps[iter].lr, steps[iter].c1, steps[iter].c2, theta[j], gcur[j], l1,
+                                       &am[j], &av[j]);
+          ++iter;
+          int maxd = 0;
+          for (int n = 0; n < N; ++n) maxd = dC[n] > maxd ? dC[n] : maxd;
+          sgm_pe_rebuild(&mo, theta, maxd + every + 1);
+          if (theta_out) memcpy(theta_out + (size_t)(t / every) * dim, theta, sizeof(double) * dim);
+        }
+        double* sw = phiP;
+        phiP = phiC;
+        phiC = sw;
+        if (mo.overflow) { rc = HYG_ENOMEM; goto done; }
+      }
       /* updatePsi (:152-197) for every pending time */
       for (int s = 0; s < npend; ++s) {
         double* ps = pend[s].psi;
@@ -364,9 +510,45 @@ done:
   free(pend);
   free(dP); free(rP); free(dC); free(rC); free(anc); free(idx);
   free(lwP); free(lwC); free(wP); free(wC); free(lwres); free(tmp); free(tmp2); free(logq); free(BK); free(cum);
+pe_fail:
+  free(theta); free(am); free(av); free(gprev); free(gcur); free(phiP); free(phiC); free(steps);
   sgm_free(&mo);
   return rc;
 #undef ADD_PENDING
+}
+
+int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t seed, uint64_t chain_id,
+                    double* probs, int32_t* nparts_out) {
+  return sg_chain_core(p, NULL, E, T, seed, chain_id, probs, nparts_out, NULL);
+}
+/* theta_out [1 + (T - 1) / every][K^2] */
+int oracle_sg_chain_pe(const hyg_sg_params* p, const hyg_sg_pe_params* pe, const double* E, int T, uint64_t seed,
+                       uint64_t chain_id, double* probs, double* theta_out) {
+  return sg_chain_core(p, pe, E, T, seed, chain_id, probs, NULL, theta_out);
+}
+int oracle_sg_pe_hazard(const hyg_sg_params* p, const double* theta, int L, hyg_sgpe_row* rows, int32_t* Lr) {
+  /* hazard rows of the estimation path for tests: rows [K][L] */
+  hyg_sg_pe_params pe = {1, 0, 200, 0, 0.1, 0.01};
+  sg_model mo;
+  int rc = sgm_init(&mo, p, L + 1);
+  if (rc) return rc;
+  rc = hyg_sgpe_consts_make(p, &pe, &mo.pc);
+  if (rc) { sgm_free(&mo); return rc; }
+  mo.pe = 1;
+  mo.rcap = L;
+  const int K = mo.c.K;
+  mo.rows = malloc(sizeof(hyg_sgpe_row) * (size_t)K * L);
+  mo.lgk = malloc(sizeof(double) * (size_t)K * L);
+  mo.h = malloc(sizeof(double) * L); mo.g = malloc(sizeof(double) * L);
+  mo.Hm1s = malloc(sizeof(double) * L); mo.gm1s = malloc(sizeof(double) * L);
+  mo.exs = malloc(L);
+  if (!mo.rows || !mo.lgk || !mo.h || !mo.g || !mo.Hm1s || !mo.gm1s || !mo.exs) { sgm_free(&mo); return HYG_ENOMEM; }
+  hyg_sgpe_lgk_fill(mo.pc.kappa, K, L, mo.lgk);
+  sgm_pe_rebuild(&mo, theta, L);
+  memcpy(rows, mo.rows, sizeof(hyg_sgpe_row) * (size_t)K * L);
+  for (int r = 0; r < K; ++r) Lr[r] = mo.Lr[r];
+  sgm_free(&mo);
+  return HYG_OK;
 }
 
 /* E[t][r] = sum_s BB(y | n, alpha_r, beta_r) (singleGroup.h:611-627, misc.h:630-640),

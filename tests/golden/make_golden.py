@@ -102,14 +102,32 @@ def sg_chain_fixture(name, K, T, S, coverage, data_seed, seed, chain_id, u, Nmax
                         meth=meth, tot=tot, regime=d["regime_control"], E=E, regime_probs=out["regime_probs"])
 
 
+def sg_pe_fixture():
+    """single-group chain with online parameter estimation (8f-1): pipeline
+    model (make_params defaults), ADAM, an update every 100 steps"""
+    T, every, seed, chain_id = 2500, 100, 4, (9 << 32) | 1
+    d = syn.simulate(T, 2, 1, K=6, coverage=15.0, seed=41, u=3, omega=0.9)
+    meth, tot = d["meth_control"], d["tot_control"]
+    p = sb.make_params(K=6)
+    out = sb.chain_pe(p, sb.make_pe(every=every), sb.emission(p, meth, tot), seed, chain_id)
+    assert out["status"] == 0
+    np.savez_compressed(os.path.join(HERE, "sg_pe_chain.npz"), every=every, seed=np.uint64(seed),
+                        chain_id=np.uint64(chain_id), meth=meth, tot=tot, regime_probs=out["regime_probs"],
+                        theta=out["theta"])
+
+
 def main():
     only_sg = "sg" in sys.argv[1:]
+    if "sg_pe" in sys.argv[1:]:
+        sg_pe_fixture()
+        return
     if not only_sg:
         for name, kw in CHAINS.items():
             chain_fixture(name, **kw)
         tables_fixture()
     for name, kw in SG_CHAINS.items():
         sg_chain_fixture(name, **kw)
+    sg_pe_fixture()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))
