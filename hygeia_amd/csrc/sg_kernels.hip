@@ -406,7 +406,8 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   for (int i = tid; i <= NT; i += NB) logm[i] = hyg_log((double)i);  // log(M - k) of the K loop
   // phase timers: 0 copy, 1 sort, 2 K loop, 3 residual / keep-top, 4 weights,
   // 5 normalise, 6 smoothing, 7 compaction; counters 8 optimal steps, 9
-  // keep-top steps, 10 K-loop iterations, 11 pending entries, 15 = last stamp
+  // keep-top steps, 10 K-loop iterations, 11 pending entries, 12 parameter
+  // estimation (phi, updates, rebuilds), 15 = last stamp
   if (tid < 16) sh.ph[tid] = 0;
 #define SG_PH(k)                                                   \
   if (dbg && tid == 0) {                                           \
@@ -724,35 +725,89 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         double* phiC = pc.phi + (size_t)cb * NT * dim;
         const double* gfrP = gfr + pb * NT;
         const uint32_t* stPP = st_ + pb * NT;
-        if (tid < M) {  // continuing particle: phi of the ancestor + the omega entry
-          const int a = anc[tid];
-          const int jr = jw + sg_r(my_st);
-          const double gcv = gct[pb * NT + a];
-          const double* src = phiP + (size_t)a * dim;
-          double* dst = phiC + (size_t)tid * dim;
-#pragma unroll 4
-          for (int j = 0; j < dim; ++j) dst[j] = src[j] + ((j == jr) ? gcv : 0.0);
+        // continuing particles: phi of the ancestor + the omega entry, one
+        // (particle, coordinate) element per thread and iteration (coalesced rows)
+        constexpr int kCb0 = (NT * dim + NB - 1) / NB;  // all elements in one round of loads (K <= 6)
+        constexpr int kCb = kCb0 < 18 ? kCb0 : 18;
+        for (int e0 = 0; e0 < M * dim; e0 += kCb * NB) {
+          double v[kCb];
+#pragma unroll
+          for (int i = 0; i < kCb; ++i) {
+            const int e = e0 + i * NB + tid;
+            const int n = e / dim, j = e - n * dim;
+            v[i] = (e < M * dim) ? phiP[(size_t)anc[n] * dim + j] : 0.0;
+          }
+#pragma unroll
+          for (int i = 0; i < kCb; ++i) {
+            const int e = e0 + i * NB + tid;
+            if (e < M * dim) {
+              const int n = e / dim, j = e - n * dim;
+              const int a = anc[n];
+              phiC[e] = v[i] + ((j == jw + sg_r(stPP[a])) ? gct[pb * NT + a] : 0.0);
+            }
+          }
         }
-        for (int pq = tid; pq < K * dim; pq += NB) {  // fresh particle (1, q), coordinate j
+        // fresh particle (1, q), coordinate j: the sum over the previous
+        // particles in kCh fixed chunks of rows (hyg_sgpe_fresh_chunks), each
+        // in n order, one (chunk, q, j) task per thread. The gradient of
+        // log f((1, q) | (d_n, r_n)) at j is nonzero only when q != r_n and
+        // d_n >= u, and then it is gomg_n if j is the omega entry of r_n
+        // (r_n == rw), or the constant -P[rb][jj] (+1 if jj == q) if j lies in
+        // the P block of r_n (r_n == rb): branch-free selects over kFb previous
+        // particles loaded at once (phi rows up to 256 exist; the ones >= Np
+        // are not used). Chunk sums meet in LDS (scr) and are added left to right.
+        constexpr int kCh = (K <= 8 ? 512 : 256) / (K * K * K) >= 8 ? 8
+                          : (K <= 8 ? 512 : 256) / (K * K * K) >= 4 ? 4
+                          : (K <= 8 ? 512 : 256) / (K * K * K) >= 2 ? 2 : 1;
+        constexpr int kRows = NT / kCh;
+        constexpr int kFb = 8;
+        double* part = (double*)(smem + lay.scr);  // [kCh][K][dim] when kCh > 1
+        for (int e = tid; e < kCh * K * dim; e += NB) {
+          const int ck = e / (K * dim), pq = e - ck * (K * dim);
           const int q = pq / dim, j = pq - q * dim;
           const int rb = (j < jw) ? j / (K - 1) : -1;
-          double acc = 0.0;
-          for (int n = 0; n < Np; ++n) {
-            const uint32_t sn = stPP[n];
-            const int rp = sg_r(sn);
-            double g = 0.0;
-            if (q != rp && sg_d(sn) >= u) {
-              if (j == jw + rp) {
-                g = gfrP[n];
-              } else if (rb == rp) {
-                const int i = j - rp * (K - 1), jj = (i < rp) ? i : i + 1;
-                g = -pm->P[rp * K + jj];
-                if (jj == q) g = g + 1.0;
-              }
-            }
-            acc = acc + BK[q * NT + n] * (phiP[(size_t)n * dim + j] + g);
+          const int rw = (j >= jw) ? j - jw : -1;
+          double cval = 0.0;
+          if (rb >= 0) {
+            const int ii = j - rb * (K - 1), jj = (ii < rb) ? ii : ii + 1;
+            cval = -pm->P[rb * K + jj];
+            if (jj == q) cval = cval + 1.0;
           }
-          phiC[(size_t)(M + q) * dim + j] = acc;
+          const double* col = phiP + j;
+          const double* bkq = BK + q * NT;
+          const int nb0 = ck * kRows, nb1 = (nb0 + kRows < Np) ? nb0 + kRows : Np;
+          double acc = 0.0;
+          for (int n0 = nb0; n0 < nb1; n0 += kFb) {
+            double v[kFb], bk[kFb], gf[kFb];
+            uint32_t sn[kFb];
+#pragma unroll
+            for (int i = 0; i < kFb; ++i) {
+              v[i] = col[(size_t)(n0 + i) * dim];
+              sn[i] = stPP[n0 + i];
+              bk[i] = bkq[n0 + i];
+              gf[i] = gfrP[n0 + i];
+            }
+#pragma unroll
+            for (int i = 0; i < kFb; ++i) {
+              const int rp = sg_r(sn[i]);
+              const bool valid = (q != rp) && (sg_d(sn[i]) >= u);
+              const double g = valid ? ((rp == rw) ? gf[i] : ((rp == rb) ? cval : 0.0)) : 0.0;
+              const double term = bk[i] * (v[i] + g);
+              acc = (n0 + i < nb1) ? acc + term : acc;
+            }
+          }
+          if (kCh == 1) phiC[(size_t)(M + q) * dim + j] = acc;
+          else part[e] = acc;
+        }
+        if (kCh > 1) {
+          lds_barrier();
+          for (int pq = tid; pq < K * dim; pq += NB) {
+            double acc = part[pq];
+#pragma unroll
+            for (int ck = 1; ck < kCh; ++ck) acc = acc + part[ck * K * dim + pq];
+            const int q = pq / dim, j = pq - q * dim;
+            phiC[(size_t)(M + q) * dim + j] = acc;
+          }
         }
         __syncthreads();
         if (t % every == 0) {
@@ -761,7 +816,14 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           const double* wCur = w_ + cb * NT;
           for (int j = tid; j < dim; j += NB) {
             double est = 0.0;
-            for (int n = 0; n < N; ++n) est = est + wCur[n] * phiC[(size_t)n * dim + j];
+            for (int n0 = 0; n0 < N; n0 += kFb) {
+              double v[kFb];
+#pragma unroll
+              for (int i = 0; i < kFb; ++i) v[i] = phiC[(size_t)(n0 + i) * dim + j];
+#pragma unroll
+              for (int i = 0; i < kFb; ++i)
+                if (n0 + i < N) est = est + wCur[n0 + i] * v[i];
+            }
             pc.gc[j] = est - pc.gp[j];
             pc.gp[j] = est;
           }
@@ -783,7 +845,10 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           // rows for every sojourn the set can reach before the next rebuild
           const int maxd = (int)block_max<NB>((tid < N) ? (double)sg_d(my_st) : 0.0, red);
           __syncthreads();
+          SG_PH(12);
           sg_pe_rebuild<NB>(pe, c, pc, pm, peLr, peEx, K, u, maxd + every + 1);
+          SG_PH(13);
+          SG_CNT(14, maxd + every + 1);
         }
         int ov = 0;
         if (tid < N) {
@@ -796,6 +861,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           status = HYG_ENOMEM;
           break;
         }
+        SG_PH(12);
       }
     }
     // ---- online marginal smoothing: updatePsi (OnlineMarginalSmoothing.h:152-197)
@@ -1055,6 +1121,11 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
       fprintf(stderr, " %s=%.0f", nm[k], v);
       sum += v;
     }
+    const double pe_c = (double)h[(size_t)lc * 16 + 12] / steps, pe_r = (double)h[(size_t)lc * 16 + 13] / steps;
+    if (pe)
+      fprintf(stderr, " estimation=%.0f rebuild=%.0f (rows/rebuild %.0f)", pe_c, pe_r,
+              (double)h[(size_t)lc * 16 + 14] / std::max(1.0, steps / (double)pe->c.every));
+    sum += pe_c + pe_r;
     fprintf(stderr, " total=%.0f | optimal=%.0f keep_top=%.0f kloop_iters/capped=%.2f pending/step=%.2f\n", sum,
             (double)h[(size_t)lc * 16 + 8], (double)h[(size_t)lc * 16 + 9],
             (double)h[(size_t)lc * 16 + 10] /

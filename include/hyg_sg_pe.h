@@ -105,25 +105,36 @@ HYG_HD void hyg_sgpe_hazard_point(const hyg_sgpe_model* m, int r, int d, int u, 
 HYG_HD int hyg_sgpe_hazard_scan(const double* h, const double* g, int u, int L, double* Hm1s, double* gm1s,
                                 uint8_t* ex) {
   double Hm1 = 0.0, gm1 = 0.0;
-  for (int d = 0; d < L; ++d) {
-    if (d < u - 1) {
-      Hm1s[d] = 0.0;
-      gm1s[d] = 0.0;
-      ex[d] = 0;
-      continue;
+  /* the inputs are read 16 rows ahead of the sequential recursion (on the GPU
+   * one lane per regime runs it: the loads then overlap) */
+  for (int d0 = 0; d0 < L; d0 += 16) {
+    double hb[16], gb[16];
+    for (int i = 0; i < 16; ++i) {
+      const int d = d0 + i;
+      hb[i] = (d < L) ? h[d] : 0.0;
+      gb[i] = (d < L) ? g[d] : 0.0;
     }
-    const double hd = h[d];
-    if (Hm1 >= 1.0) { /* exit onset: bigH[d-1] is overwritten with 0.99999 */
-      Hm1s[d] = HYG_SGPE_EXIT_H;
+    for (int i = 0; i < 16; ++i) {
+      const int d = d0 + i;
+      if (d >= L) break;
+      if (d < u - 1) {
+        Hm1s[d] = 0.0;
+        gm1s[d] = 0.0;
+        ex[d] = 0;
+        continue;
+      }
+      if (Hm1 >= 1.0) { /* exit onset: bigH[d-1] is overwritten with 0.99999 */
+        Hm1s[d] = HYG_SGPE_EXIT_H;
+        gm1s[d] = gm1;
+        ex[d] = 1;
+        return d + 1;
+      }
+      Hm1s[d] = Hm1;
       gm1s[d] = gm1;
-      ex[d] = 1;
-      return d + 1;
+      ex[d] = 0;
+      Hm1 = Hm1 + hb[i];
+      gm1 = gm1 + hb[i] * gb[i];
     }
-    Hm1s[d] = Hm1;
-    gm1s[d] = gm1;
-    ex[d] = 0;
-    Hm1 = Hm1 + hd;
-    gm1 = gm1 + hd * g[d];
   }
   return L;
 }
@@ -153,6 +164,19 @@ HYG_HD hyg_sgpe_row hyg_sgpe_hazard_row(double h, double g, double Hm1, double g
   o.gomg = gomg;
   o.gcont = (!exd && rho < 1.0) ? ((-gomg) * rho) / (1.0 - rho) : 0.0;
   return o;
+}
+
+/* The fresh particle's phi (OnlineParameterEstimation.h:136-144) sums K_q(n)
+ * (phi_n + grad_qn) over the previous particles n. The sum is taken in C
+ * fixed chunks of 256 / C rows, each summed in n order, the chunk sums then
+ * added left to right (C = 1: the reference's sequential order). C spreads
+ * the K x K^2 sums over the threads of the chain's workgroup (512 threads
+ * for K <= 8, 256 above): C = the largest power of two <= threads / K^3,
+ * at most 8. */
+HYG_HD int hyg_sgpe_fresh_chunks(int K) {
+  const int nb = (K <= 8) ? 512 : 256;
+  const int c = nb / (K * K * K);
+  return c >= 8 ? 8 : (c >= 4 ? 4 : (c >= 2 ? 2 : 1));
 }
 
 /* ADAM / gradient-ascent step sizes (GradientAscent.h:124-127,147): per

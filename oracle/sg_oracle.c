@@ -415,10 +415,14 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
           for (int j = 0; j < dim; ++j)
             phiC[(size_t)n * dim + j] = phiP[(size_t)a * dim + j] + ((j == jw + rC[n]) ? w->gcont : 0.0);
         }
+        const int nch = hyg_sgpe_fresh_chunks(K), rows = 256 / nch;
         for (int q = 0; q < K; ++q) {
           for (int j = 0; j < dim; ++j) {
             double acc = 0.0;
-            for (int n = 0; n < Np; ++n) {
+            for (int ck = 0; ck < nch; ++ck) {
+            double part = 0.0;
+            const int n1 = (ck + 1) * rows < Np ? (ck + 1) * rows : Np;
+            for (int n = ck * rows; n < n1; ++n) {
               const int rp = rP[n];
               double g = 0.0;
               if (q != rp && dP[n] >= c->u) {
@@ -430,7 +434,9 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
                   if (jj == q) g = g + 1.0;
                 }
               }
-              acc = acc + BK[q * Nmax + n] * (phiP[(size_t)n * dim + j] + g);
+              part = part + BK[q * Nmax + n] * (phiP[(size_t)n * dim + j] + g);
+            }
+            acc = (ck == 0) ? part : acc + part;
             }
             phiC[(size_t)(M + q) * dim + j] = acc;
           }

@@ -7,6 +7,11 @@ resident in HBM. Prints one JSON line in bench.py's format (units = CpG sites).
 
     python tools/bench_sg.py [--sites N] [--steps K] [--warmup W] [--per-sample]
 
+--estimate-parameters runs the two-group pipeline's actual stage 2
+(2_estimate_parameters_and_regimes.nf: --estimate_regime_probabilities
+--estimate_parameters): online parameter estimation with the
+flag defaults (ADAM, an update every 200 steps), theta rows written per chain.
+
 --per-sample runs the single-group pipeline's granularity instead
 (modules/single_group/3_estimate_regimes.nf: one process per (case_id,
 chromosome), one sample per chain): samples x 22 chains of S = 1, units = CpG
@@ -38,14 +43,19 @@ def bytes_per_site(S: int, K: int) -> int:
     return 4 * S + 16 * K + 8 * K
 
 
-def cpu_baseline(meth, tot, chains, params, seconds, threads):
+def cpu_baseline(meth, tot, chains, params, seconds, threads, pe=False):
     from oracle import sg_binding as sb
 
     p = sb.SgParams.from_buffer_copy(bytes(params))
+    ope = sb.make_pe()
+
+    def run(E, seed, cid):
+        return sb.chain_pe(p, ope, E, seed, cid) if pe else sb.chain(p, E, seed, cid)
+
     s0 = chains[0][0]
     n_cal = 2000
     t0 = time.perf_counter()
-    sb.chain(p, sb.emission(p, meth[s0:s0 + n_cal], tot[s0:s0 + n_cal]), 0, 1)
+    run(sb.emission(p, meth[s0:s0 + n_cal], tot[s0:s0 + n_cal]), 0, 1)
     per_site = (time.perf_counter() - t0) / n_cal
     n = int(max(2000, min(400000, seconds / per_site)))
     res = [0] * threads
@@ -53,7 +63,7 @@ def cpu_baseline(meth, tot, chains, params, seconds, threads):
     def work(i):
         b = chains[i % len(chains)][0]
         sl = slice(b, b + n)
-        out = sb.chain(p, sb.emission(p, meth[sl], tot[sl]), i, 7 + i)
+        out = run(sb.emission(p, meth[sl], tot[sl]), i, 7 + i)
         assert out["status"] == 0
         res[i] = n
 
@@ -66,7 +76,8 @@ def cpu_baseline(meth, tot, chains, params, seconds, threads):
     dt = time.perf_counter() - t0
     return {"value": sum(res) / dt, "unit": "CpG-sites/s", "cores": threads, "kind": "port",
             "sample": f"{threads} threads x {n}-site prefixes of the chromosome chains, each one "
-                      f"oracle/sg_oracle.c emission + SMC + online smoothing; {sum(res)} sites in {dt:.1f} s"}
+                      f"oracle/sg_oracle.c emission + SMC + online smoothing"
+                      f"{' + online parameter estimation' if pe else ''}; {sum(res)} sites in {dt:.1f} s"}
 
 
 def main():
@@ -82,6 +93,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--per-sample", action="store_true", help="one chain per (sample, chromosome), S = 1")
+    ap.add_argument("--estimate-parameters", action="store_true", help="online parameter estimation (8f-1)")
     args = ap.parse_args()
 
     import torch
@@ -127,7 +139,15 @@ def main():
         raise SystemExit("the C2 workload is K = 6")
     h = C.c_void_p()
     _lib.check(L.hyg_sg_model_create(C.byref(p), max_reads, int(max(sizes)), C.byref(h)))
-    wsb = int(L.hyg_sg_workspace_bytes(h, len(chains), args.psi_capacity))
+    pe = None
+    if args.estimate_parameters:
+        pe = _lib.SgPeParams()
+        L.hyg_sg_pe_params_default(C.byref(pe))
+        n_theta = int(L.hyg_sg_pe_theta_rows(arr, len(chains), pe.n_steps_without_update))
+        theta = torch.empty((n_theta, K * K), dtype=torch.float64, device=dev)
+        wsb = int(L.hyg_sg_pe_workspace_bytes(h, arr, len(chains), args.psi_capacity))
+    else:
+        wsb = int(L.hyg_sg_workspace_bytes(h, len(chains), args.psi_capacity))
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     E = torch.empty((n_rows, K), dtype=torch.float64, device=dev)
     probs = torch.empty((n_rows, K), dtype=torch.float64, device=dev)
@@ -141,8 +161,13 @@ def main():
         ev[0].record(stream)
         _lib.check(L.hyg_sg_emission(h, meth.data_ptr(), tot.data_ptr(), S, n_rows, E.data_ptr(), sp))
         ev[1].record(stream)
-        _lib.check(L.hyg_sg_run_chains(h, arr, len(chains), E.data_ptr(), ws.data_ptr(), wsb, args.psi_capacity,
-                                       probs.data_ptr(), st.data_ptr(), sp))
+        if pe is not None:
+            _lib.check(L.hyg_sg_run_chains_pe(h, C.byref(pe), arr, len(chains), E.data_ptr(), ws.data_ptr(), wsb,
+                                              args.psi_capacity, probs.data_ptr(), theta.data_ptr(), st.data_ptr(),
+                                              sp))
+        else:
+            _lib.check(L.hyg_sg_run_chains(h, arr, len(chains), E.data_ptr(), ws.data_ptr(), wsb,
+                                           args.psi_capacity, probs.data_ptr(), st.data_ptr(), sp))
         ev[2].record(stream)
         if timed:
             ev[2].synchronize()
@@ -170,19 +195,24 @@ def main():
         print("bad rows:", len(idx), "first:", idx[:10].tolist(), "chains:", owner,
               "values:", probs[torch.from_numpy(idx[:3]).to(dev)].cpu().numpy().tolist(), file=sys.stderr)
         raise RuntimeError("regime probabilities do not sum to one")
+    if pe is not None and not bool(torch.isfinite(theta).all().item()):
+        raise RuntimeError("non-finite theta estimates")
     ms = dt * 1000.0 / args.steps
     kavg = kms / args.steps
     bps = bytes_per_site(S, K)
     units = n_rows  # CpG sites (joint chains) or sites x samples (per-sample chains)
     line = {
-        "metric": "CpG sites/sec through SMC + online smoothing (single group)", "value": units / (ms / 1000.0),
+        "metric": "CpG sites/sec through SMC + online smoothing (single group)"
+                  + (" + online parameter estimation" if pe is not None else ""), "value": units / (ms / 1000.0),
         "unit": "CpG-site-samples/s" if args.per_sample else "CpG-sites/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": (f"C2 single_group {args.sites} CpG x {args.samples} samples, one chain per "
                                 f"(sample, chromosome) = {len(chains)} chains of 1 sample" if args.per_sample else
                                 f"C2 single_group {args.sites} CpG, 22 chromosome chains, {S} samples jointly")
-                               + f", K={K}, N_max=250, epsilon=0.01, 1 seed, coverage {args.coverage}",
+                               + f", K={K}, N_max=250, epsilon=0.01, 1 seed, coverage {args.coverage}"
+                               + (", online parameter estimation (ADAM, update every 200 steps)"
+                                  if pe is not None else ""),
                    "chains": len(chains), "longest_chain": int(max(sizes)), "parallelism": "chains on 1 GPU"},
         "roofline": {"bound": "hbm", "kernel": "sg_chain_kernel",
                      "achieved": bps * units / (kavg[1] / 1000.0) / 1e9, "peak": HBM_PEAK_GBS,
@@ -193,7 +223,7 @@ def main():
     }
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(meth.cpu().numpy().view(np.uint16), tot.cpu().numpy().view(np.uint16),
-                                            chains, p, args.cpu_seconds, args.cpu_threads)
+                                            chains, p, args.cpu_seconds, args.cpu_threads, pe=pe is not None)
         line["cpu_baseline"]["unit"] = line["unit"]
     L.hyg_sg_model_destroy(h)
     print(json.dumps(line), flush=True)
