@@ -279,14 +279,26 @@ def main(argv: Sequence[str] = None) -> int:
         except FlagError as e:
             print(f"FATAL Flags parsing error: {e}", file=sys.stderr)
             return 1
+    if cmd == "get_chrom_segments":
+        from . import bed
+        try:
+            return bed.get_chrom_segments_main(rest)
+        except FlagError as e:
+            print(f"FATAL Flags parsing error: {e}", file=sys.stderr)
+            return 1
+    if cmd == "make_bed_file":  # the single-group container's subcommand
+        from . import bed
+        return bed.make_bed_file_main(rest)
     if cmd in ("version", "-v", "--version"):
         from . import _lib
         print("Hygeia version {} ({})".format(os.environ.get("HYGEIA_VERSION", ""),
                                               _lib.load().hyg_version().decode()))
         return 0
     if cmd in ("help", "-h", "--help"):
-        print("Usage: hygeia [command] [arguments...]\n  infer     - Run inference on two groups (MI355X)\n"
-              "  aggregate - Aggregate results\n  get_dmps  - Get DMPs (Differentially Methylated Positions)")
+        print("Usage: hygeia [command] [arguments...]\n  get_chrom_segments - Get chromosome segments\n"
+              "  infer     - Run inference on two groups (MI355X)\n"
+              "  aggregate - Aggregate results\n  get_dmps  - Get DMPs (Differentially Methylated Positions)\n"
+              "  make_bed_file - Regime BED track of a single-group regimes CSV (MI355X)")
         return 0
     if cmd in COMMANDS.split():
         print(f"Error: '{cmd}' is not part of the MI355X inference path; use the reference pipeline step",

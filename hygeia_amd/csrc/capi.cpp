@@ -17,6 +17,10 @@
 #include "tg_common.h"
 #include "dmp_common.h"
 
+namespace hyg {
+int bed_launch_labels(const double* probs, int K, int64_t n, int8_t* label, double* score, void* stream);
+}
+
 using namespace hyg;
 
 namespace {
@@ -671,6 +675,47 @@ int hyg_sg_run_chain_host_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, 
   if (st == HYG_ENOMEM) return fail(st, "pending smoothing times exceeded psi_capacity, or a sojourn outgrew the hazard rows");
   if (st != HYG_OK) return fail(st, "all particle weights became -inf");
   return HYG_OK;
+}
+
+// ---- regime BED tracks
+
+int hyg_bed_labels(const double* probs, int32_t K, int64_t n, int8_t* label, double* score, void* stream) {
+  if (K < 1 || K > HYG_KMAX || n < 0) return fail(HYG_EINVAL, "K out of [1, 16] or negative n_sites");
+  if (n > 0 && (!probs || !label || !score)) return fail(HYG_EINVAL, "null buffer");
+  if (!have_device()) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  const int rc = bed_launch_labels(probs, K, n, label, score, stream);
+  if (rc != HYG_OK) return fail(rc, "label launch failed");
+  return HYG_OK;
+}
+
+int64_t hyg_bed_format(const char* chrom, const int64_t* pos, const int8_t* label, const double* score, int64_t n,
+                       int32_t K, const char* const* names, const char* const* rgb, char* out, int64_t out_bytes) {
+  if (!chrom || K < 1 || K > HYG_KMAX || n < 0 || !names || !rgb) return fail(HYG_EINVAL, "invalid argument");
+  if (n > 0 && (!pos || !label || !score)) return fail(HYG_EINVAL, "null buffer");
+  for (int r = 0; r <= K; ++r)
+    if (!names[r] || !rgb[r]) return fail(HYG_EINVAL, "null name or colour");
+  int64_t need = 0;
+  char line[512];
+  for (int64_t i = 0; i < n; ++i) {
+    const int lb = label[i];
+    if (lb < -1 || lb >= K) return fail(HYG_EINVAL, "label out of range");
+    const int k = lb < 0 ? K : lb;
+    char sc[64];
+    // fwrite(scipen = 999): fixed notation, <= 15 significant digits, no trailing zeros
+    int m = std::snprintf(sc, sizeof sc, "%.15g", score[i]);
+    if (std::strchr(sc, 'e')) {  // tiny or huge values: positional form of the same digits
+      m = std::snprintf(sc, sizeof sc, "%.17f", score[i]);
+      while (m > 1 && sc[m - 1] == '0') sc[--m] = 0;
+      if (m > 1 && sc[m - 1] == '.') sc[--m] = 0;
+    }
+    const long long a = (long long)pos[i] - 1, b = (long long)pos[i] + 1;
+    const int len = std::snprintf(line, sizeof line, "%s\t%lld\t%lld\t%s\t%s\t.\t%lld\t%lld\t%s\n", chrom, a, b,
+                                  names[k], sc, a, b, rgb[k]);
+    if (len < 0 || len >= (int)sizeof line) return fail(HYG_EINVAL, "BED line too long");
+    if (out && need + len <= out_bytes) std::memcpy(out + need, line, (size_t)len);
+    need += len;
+  }
+  return need;
 }
 
 }  // extern "C"

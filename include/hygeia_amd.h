@@ -312,6 +312,27 @@ int hyg_dmp_weighted_fdr(const int32_t* counts, int32_t stride, int32_t column, 
                          double fdr_threshold, const double* w_fp, const double* w_fn, int64_t* ranked,
                          int64_t* s, double* n_sum, void* stream);
 
+/* ================================================ regime BED tracks
+ * make_bed_file (src/single_group/bin/make_bed_file:19-66)
+ * on regime probabilities resident in HBM. */
+
+/* Per site of regime_probs [n_sites][K] f64 (device): score = the largest
+ * probability, label = the first regime attaining it, or -1 ("equiprobable")
+ * when more than one does (data.table pmax / rowSums(.SD == score) / max.col
+ * ties.method "first"). label [n_sites] int8, score [n_sites] f64 (device). */
+int hyg_bed_labels(const double* regime_probs, int32_t K, int64_t n_sites, int8_t* label, double* score,
+                   void* stream);
+/* Host: the BED lines of fwrite(bed, sep = "\t", col.names = FALSE, scipen = 999)
+ *   chrom  pos-1  pos+1  name  score  .  pos-1  pos+1  itemRgb
+ * for sites already in output order (setkey(bed, chr, start)); names[K + 1]
+ * = the regime column names then "equiprobable", rgb[K + 1] likewise; score
+ * with at most 15 significant digits, trailing zeros dropped. Writes at most
+ * out_bytes bytes; returns the bytes needed (call with out = NULL to size the
+ * buffer) or a negative HYG_E* code. */
+int64_t hyg_bed_format(const char* chrom, const int64_t* positions, const int8_t* label, const double* score,
+                       int64_t n_sites, int32_t K, const char* const* names, const char* const* rgb, char* out,
+                       int64_t out_bytes);
+
 /* Number of visible HIP devices (0 when none: compute calls then fail). */
 int hyg_device_count(void);
 const char* hyg_last_error(void);
