@@ -118,7 +118,7 @@ EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy
            "hyg_sg_params_default", "hyg_sg_model_create", "hyg_sg_model_destroy", "hyg_sg_emission",
            "hyg_sg_workspace_bytes", "hyg_sg_run_chains", "hyg_sg_run_chain_host",
            "hyg_sg_pe_params_default", "hyg_sg_pe_theta_rows", "hyg_sg_pe_workspace_bytes", "hyg_sg_run_chains_pe",
-           "hyg_sg_run_chain_host_pe", "hyg_bed_labels", "hyg_bed_format",
+           "hyg_sg_run_chain_host_pe", "hyg_bed_labels", "hyg_bed_format", "hyg_pre_collapse",
            "hyg_dmp_site_counts", "hyg_dmp_fdr", "hyg_dmp_weighted_fdr")
 
 
@@ -195,6 +195,8 @@ def load() -> C.CDLL:
     L.hyg_sg_run_chains_pe.restype = C.c_int
     L.hyg_sg_run_chains_pe.argtypes = [vp, C.POINTER(SgPeParams), C.POINTER(SgChain), i32, vp, vp, sz, i32, vp, vp,
                                        vp, vp]
+    L.hyg_pre_collapse.restype = C.c_int
+    L.hyg_pre_collapse.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, vp, vp]
     L.hyg_bed_labels.restype = C.c_int
     L.hyg_bed_labels.argtypes = [vp, i32, i64, vp, vp, vp]
     L.hyg_bed_format.restype = i64

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libhygeia_amd.so")
-SOURCES = [os.path.join(HERE, "csrc", f) for f in ("capi.cpp", "tg_kernels.hip", "sg_kernels.hip", "dmp_kernels.hip", "bed_kernels.hip")]
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("capi.cpp", "tg_kernels.hip", "sg_kernels.hip", "dmp_kernels.hip", "bed_kernels.hip", "pre_kernels.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in ("tg_common.h", "sg_common.h", "dmp_common.h", "hyg_dev.h")] + [
     os.path.join(ROOT, "include", f) for f in ("hygeia_amd.h", "hyg_arith.h", "hyg_model.h", "hyg_sg_model.h", "hyg_sg_pe.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

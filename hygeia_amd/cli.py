@@ -111,6 +111,8 @@ def parse_flags(argv: Sequence[str], flags_spec=None) -> Dict[str, object]:
                 out[name] = [x for x in val.split(",") if x != ""]
             elif kind == "multi_int":
                 multi.setdefault(name, []).extend(int(x) for x in val.split(","))
+            elif kind == "multi_string":
+                multi.setdefault(name, []).append(val)
             elif kind == "multi_float":
                 multi.setdefault(name, []).extend(float(x) for x in val.split(","))
             else:
@@ -279,6 +281,13 @@ def main(argv: Sequence[str] = None) -> int:
         except FlagError as e:
             print(f"FATAL Flags parsing error: {e}", file=sys.stderr)
             return 1
+    if cmd == "preprocess":
+        from . import preprocess
+        try:
+            return preprocess.main(rest)
+        except FlagError as e:
+            print(f"FATAL Flags parsing error: {e}", file=sys.stderr)
+            return 1
     if cmd == "get_chrom_segments":
         from . import bed
         try:
@@ -295,7 +304,8 @@ def main(argv: Sequence[str] = None) -> int:
                                               _lib.load().hyg_version().decode()))
         return 0
     if cmd in ("help", "-h", "--help"):
-        print("Usage: hygeia [command] [arguments...]\n  get_chrom_segments - Get chromosome segments\n"
+        print("Usage: hygeia [command] [arguments...]\n  preprocess - Preprocess BED methylation files (MI355X)\n"
+              "  get_chrom_segments - Get chromosome segments\n"
               "  infer     - Run inference on two groups (MI355X)\n"
               "  aggregate - Aggregate results\n  get_dmps  - Get DMPs (Differentially Methylated Positions)\n"
               "  make_bed_file - Regime BED track of a single-group regimes CSV (MI355X)")

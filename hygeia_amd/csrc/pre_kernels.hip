@@ -1,0 +1,117 @@
+// pre_kernels.hip -- `hygeia preprocess`: strand collapse of
+// per-strand methylation BED records and their counts on the chromosome's CpG
+// grid, for one sample.
+//
+// Reference: src/two_group/preprocess_bed.py (polars 1.8.2)
+//   collapse_strands :183-259   full join of "+" rows (key end) with "-" rows
+//                               (key start); coverage / percent of a missing
+//                               strand 0; total = cov+ + cov-; key = start+ or
+//                               start- - 1; rows with total > 0 kept;
+//                               avg = (cov+ pct+ + cov- pct-) / total
+//   process_sample_data :298-317 meth = round(total avg / 100),
+//                               unmeth = round(total (100 - avg) / 100)
+//   :325-336, :497-543          full joins on Pos0 whose unmatched sample rows
+//                               get a null Pos0 and are dropped (:365-369): a
+//                               left join onto the CpG positions, missing -> 0
+//                               (np.nan_to_num, :384)
+// Both strands' records are sorted by start with unique starts (the host
+// checks), so the joins are binary searches: pre_mark_kernel marks the "-"
+// records a "+" record pairs with; pre_grid_kernel resolves every CpG site
+// independently (HBM-bound: a few searches and one output pair per site).
+#include <hip/hip_runtime.h>
+
+#include "../../include/hygeia_amd.h"
+
+namespace hyg {
+
+__device__ __forceinline__ int64_t pre_find(const int64_t* __restrict__ a, int64_t n, int64_t key) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return (lo < n && a[lo] == key) ? lo : -1;
+}
+
+// polars f64 round (Rust f64::round: half away from zero)
+__device__ __forceinline__ double pre_round(double x) {
+  const double a = fabs(x);
+  double f = floor(a);
+  f = (a - f >= 0.5) ? f + 1.0 : f;
+  return copysign(f, x);
+}
+
+__global__ void __launch_bounds__(256)
+pre_mark_kernel(const int64_t* __restrict__ plus_end, int64_t n_plus, const int64_t* __restrict__ minus_start,
+                int64_t n_minus, uint8_t* __restrict__ matched) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_plus; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = pre_find(minus_start, n_minus, plus_end[i]);
+    if (j >= 0) matched[j] = 1;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+pre_grid_kernel(const int64_t* __restrict__ pos0, int64_t T, const int64_t* __restrict__ plus_start,
+                const int64_t* __restrict__ plus_end, const double* __restrict__ plus_cov,
+                const double* __restrict__ plus_pct, int64_t n_plus, const int64_t* __restrict__ minus_start,
+                const double* __restrict__ minus_cov, const double* __restrict__ minus_pct, int64_t n_minus,
+                const uint8_t* __restrict__ matched, double* __restrict__ out, int stride, int col,
+                int* __restrict__ conflicts) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = pos0[t];
+    // the collapsed row with key k: a "+" record starting at k (with its "-"
+    // partner starting at its end), or an unpaired "-" record starting at k + 1
+    const int64_t ip = pre_find(plus_start, n_plus, k);
+    const int64_t jm = pre_find(minus_start, n_minus, k + 1);
+    const bool minus_only = jm >= 0 && !matched[jm];
+    double cp = 0.0, pp = 0.0, cn = 0.0, pn = 0.0;
+    bool have = false;
+    if (ip >= 0) {
+      cp = plus_cov[ip];
+      pp = plus_pct[ip];
+      const int64_t jn = pre_find(minus_start, n_minus, plus_end[ip]);
+      if (jn >= 0) {
+        cn = minus_cov[jn];
+        pn = minus_pct[jn];
+      }
+      have = true;
+      if (minus_only) atomicAdd(conflicts, 1);  // two collapsed rows with one key
+    } else if (minus_only) {
+      cn = minus_cov[jm];
+      pn = minus_pct[jm];
+      have = true;
+    }
+    const double total = cp + cn;
+    // no collapsed row (or coverage 0, filtered at :228-230): null, i.e. NaN
+    double meth = __builtin_nan(""), unmeth = __builtin_nan("");
+    if (have && total > 0.0) {
+      const double avg = ((cp * pp) + (cn * pn)) / total;
+      meth = pre_round((total * avg) / 100.0);
+      unmeth = pre_round((total * (100.0 - avg)) / 100.0);
+    }
+    out[t * stride + col] = meth;
+    out[t * stride + col + 1] = unmeth;
+  }
+}
+
+int pre_launch_collapse(const int64_t* pos0, int64_t T, const int64_t* plus_start, const int64_t* plus_end,
+                        const double* plus_cov, const double* plus_pct, int64_t n_plus, const int64_t* minus_start,
+                        const double* minus_cov, const double* minus_pct, int64_t n_minus, uint8_t* matched,
+                        double* out, int stride, int col, int* conflicts, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n_minus > 0 && hipMemsetAsync(matched, 0, (size_t)n_minus, s) != hipSuccess) return HYG_EDEVICE;
+  auto grid = [](int64_t n) {
+    int64_t b = (n + 255) / 256;
+    return (unsigned)(b < 1 ? 1 : (b > 256 * 32 ? 256 * 32 : b));
+  };
+  if (n_plus > 0 && n_minus > 0)
+    hipLaunchKernelGGL(pre_mark_kernel, dim3(grid(n_plus)), dim3(256), 0, s, plus_end, n_plus, minus_start, n_minus,
+                       matched);
+  if (T > 0)
+    hipLaunchKernelGGL(pre_grid_kernel, dim3(grid(T)), dim3(256), 0, s, pos0, T, plus_start, plus_end, plus_cov,
+                       plus_pct, n_plus, minus_start, minus_cov, minus_pct, n_minus, matched, out, stride, col,
+                       conflicts);
+  return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
+}
+
+}  // namespace hyg

@@ -333,6 +333,24 @@ int64_t hyg_bed_format(const char* chrom, const int64_t* positions, const int8_t
                        int64_t n_sites, int32_t K, const char* const* names, const char* const* rgb, char* out,
                        int64_t out_bytes);
 
+/* ================================================ preprocess (BED -> counts)
+ * `hygeia preprocess` (src/two_group/preprocess_bed.py), the
+ * device part for one sample on one chromosome: the strand collapse
+ * (collapse_strands :183-259: "+" rows joined to "-" rows on end == start,
+ * missing strand 0, key = start+ or start- - 1, rows with coverage > 0) and its
+ * counts on the CpG grid (:298-336: meth = round(total avg / 100), unmeth =
+ * round(total (100 - avg) / 100), half away from zero as polars; sites without
+ * a collapsed row NaN, the reference's null). Device pointers; each strand's records sorted by start
+ * with unique starts (the caller checks); coverage and percent as f64.
+ * Writes counts[t * stride + column] = meth, [.. + 1] = unmeth for every site;
+ * scratch [n_minus] bytes; *conflicts (device int, caller-zeroed) counts sites
+ * that two collapsed rows claim (records longer than one base). */
+int hyg_pre_collapse(const int64_t* cpg_pos0, int64_t n_sites, const int64_t* plus_start, const int64_t* plus_end,
+                     const double* plus_coverage, const double* plus_percent, int64_t n_plus,
+                     const int64_t* minus_start, const double* minus_coverage, const double* minus_percent,
+                     int64_t n_minus, uint8_t* scratch, double* counts, int32_t stride, int32_t column,
+                     int32_t* conflicts, void* stream);
+
 /* Number of visible HIP devices (0 when none: compute calls then fail). */
 int hyg_device_count(void);
 const char* hyg_last_error(void);
