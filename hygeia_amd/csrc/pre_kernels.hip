@@ -24,13 +24,20 @@
 
 namespace hyg {
 
-__device__ __forceinline__ int64_t pre_find(const int64_t* __restrict__ a, int64_t n, int64_t key) {
-  int64_t lo = 0, hi = n;
+__device__ __forceinline__ int64_t pre_lower(const int64_t* a, int64_t lo, int64_t hi, int64_t key) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
     if (a[mid] < key) lo = mid + 1; else hi = mid;
   }
-  return (lo < n && a[lo] == key) ? lo : -1;
+  return lo;
+}
+// index of key in a[lo, hi) (sorted, unique), or -1
+__device__ __forceinline__ int64_t pre_find_in(const int64_t* a, int64_t lo, int64_t hi, int64_t key) {
+  const int64_t i = pre_lower(a, lo, hi, key);
+  return (i < hi && a[i] == key) ? i : -1;
+}
+__device__ __forceinline__ int64_t pre_find(const int64_t* __restrict__ a, int64_t n, int64_t key) {
+  return pre_find_in(a, 0, n, key);
 }
 
 // polars f64 round (Rust f64::round: half away from zero)
@@ -41,15 +48,34 @@ __device__ __forceinline__ double pre_round(double x) {
   return copysign(f, x);
 }
 
+// "-" records paired with a "+" record (matched on end == start): one chunk
+// of 256 "+" records per block and iteration, searches bounded to the "-"
+// records between the chunk's first and last end when the end lies there.
 __global__ void __launch_bounds__(256)
 pre_mark_kernel(const int64_t* __restrict__ plus_end, int64_t n_plus, const int64_t* __restrict__ minus_start,
                 int64_t n_minus, uint8_t* __restrict__ matched) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_plus; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t j = pre_find(minus_start, n_minus, plus_end[i]);
+  __shared__ int64_t win[2];
+  const int64_t n_chunks = (n_plus + 255) / 256;
+  for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    const int64_t i0 = c * 256, i1 = (i0 + 256 < n_plus) ? i0 + 256 : n_plus;
+    __syncthreads();
+    if (threadIdx.x == 0) win[0] = pre_lower(minus_start, 0, n_minus, plus_end[i0]);
+    else if (threadIdx.x == 64) win[1] = pre_lower(minus_start, 0, n_minus, plus_end[i1 - 1] + 1);
+    __syncthreads();
+    const int64_t i = i0 + threadIdx.x;
+    if (i >= n_plus) continue;
+    const int64_t e = plus_end[i];
+    const int64_t lo = win[0], hi = win[1];
+    const bool inwin = lo < hi && e >= minus_start[lo] && e <= minus_start[hi - 1];
+    const int64_t j = inwin ? pre_find_in(minus_start, lo, hi, e) : pre_find(minus_start, n_minus, e);
     if (j >= 0) matched[j] = 1;
   }
 }
 
+// One 256-site chunk of the (sorted) grid per block and iteration: the
+// chunk's key range bounds every search to the records inside it (found once
+// per chunk by two threads), so a site's searches touch a few cache lines
+// instead of ~25 random ones per search over the whole chromosome.
 __global__ void __launch_bounds__(256)
 pre_grid_kernel(const int64_t* __restrict__ pos0, int64_t T, const int64_t* __restrict__ plus_start,
                 const int64_t* __restrict__ plus_end, const double* __restrict__ plus_cov,
@@ -57,19 +83,63 @@ pre_grid_kernel(const int64_t* __restrict__ pos0, int64_t T, const int64_t* __re
                 const double* __restrict__ minus_cov, const double* __restrict__ minus_pct, int64_t n_minus,
                 const uint8_t* __restrict__ matched, double* __restrict__ out, int stride, int col,
                 int* __restrict__ conflicts) {
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (int64_t)gridDim.x * blockDim.x) {
+  constexpr int kWin = 1024;
+  __shared__ int64_t win[4];  // plus [lo, hi), minus [lo, hi) of the chunk
+  __shared__ int64_t sp[kWin], sm[kWin];
+  const int64_t n_chunks = (T + 255) / 256;
+  for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    const int64_t t0 = c * 256, t1 = (t0 + 256 < T) ? t0 + 256 : T;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      win[0] = pre_lower(plus_start, 0, n_plus, pos0[t0]);
+      win[2] = pre_lower(minus_start, 0, n_minus, pos0[t0] + 1);
+    } else if (threadIdx.x == 64) {
+      win[1] = pre_lower(plus_start, 0, n_plus, pos0[t1 - 1] + 1);
+      win[3] = pre_lower(minus_start, 0, n_minus, pos0[t1 - 1] + 2);
+    }
+    __syncthreads();
+    // the windows' starts staged in LDS with coalesced loads (windows larger
+    // than kWin records -- records between grid sites -- search HBM instead)
+    const int64_t np_w = win[1] - win[0], nm_w = win[3] - win[2];
+    const bool lp = np_w <= kWin, lm = nm_w <= kWin;
+    if (lp)
+      for (int64_t i = threadIdx.x; i < np_w; i += 256) sp[i] = plus_start[win[0] + i];
+    if (lm)
+      for (int64_t i = threadIdx.x; i < nm_w; i += 256) sm[i] = minus_start[win[2] + i];
+    __syncthreads();
+    const int64_t t = t0 + threadIdx.x;
+    if (t >= T) continue;
     const int64_t k = pos0[t];
     // the collapsed row with key k: a "+" record starting at k (with its "-"
     // partner starting at its end), or an unpaired "-" record starting at k + 1
-    const int64_t ip = pre_find(plus_start, n_plus, k);
-    const int64_t jm = pre_find(minus_start, n_minus, k + 1);
+    int64_t ip, jm;
+    if (lp) {
+      ip = pre_find_in(sp, 0, np_w, k);
+      ip = ip >= 0 ? win[0] + ip : -1;
+    } else {
+      ip = pre_find_in(plus_start, win[0], win[1], k);
+    }
+    if (lm) {
+      jm = pre_find_in(sm, 0, nm_w, k + 1);
+      jm = jm >= 0 ? win[2] + jm : -1;
+    } else {
+      jm = pre_find_in(minus_start, win[2], win[3], k + 1);
+    }
     const bool minus_only = jm >= 0 && !matched[jm];
     double cp = 0.0, pp = 0.0, cn = 0.0, pn = 0.0;
     bool have = false;
     if (ip >= 0) {
       cp = plus_cov[ip];
       pp = plus_pct[ip];
-      const int64_t jn = pre_find(minus_start, n_minus, plus_end[ip]);
+      const int64_t e = plus_end[ip];
+      // the partner usually lies in the chunk's window (single-base records)
+      int64_t jn;
+      if (lm && nm_w > 0 && e >= sm[0] && e <= sm[nm_w - 1]) {
+        jn = pre_find_in(sm, 0, nm_w, e);
+        jn = jn >= 0 ? win[2] + jn : -1;
+      } else {
+        jn = pre_find(minus_start, n_minus, e);
+      }
       if (jn >= 0) {
         cn = minus_cov[jn];
         pn = minus_pct[jn];
