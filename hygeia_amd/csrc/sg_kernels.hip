@@ -96,7 +96,8 @@ struct SgShared {
 struct SgLay {
   size_t st, lw, w, base, cont;  // [2][NT]: current / previous particle sets, alternating per step
   size_t anc, lwres, logq, sidx, cum, xk, xi, BK, logP, red, lsev, scr, meanb, okb, logm, logQ, psil, sh, total;
-  size_t pm, gfr, gct, pei;  // parameter estimation: model, per-particle gradient entries [2][NT], ints
+  size_t pm, gfr, gct, pei, rpu;  // parameter estimation: model, per-particle gradient entries [2][NT], ints,
+                                  // regime if d >= u else -1 [2][NT] (int8)
   int nl;  // psi slots resident in LDS (slot ids 0 .. nl-1; the rest live in the workspace)
 };
 
@@ -137,6 +138,7 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap, bool pe) {
     l.gfr = o; o = sg_align(o + 8 * 2 * NT);
     l.gct = o; o = sg_align(o + 8 * 2 * NT);
     l.pei = o; o = sg_align(o + 4 * (2 * HYG_KMAX + 8));
+    l.rpu = o; o = sg_align(o + 2 * NT);
   }
   const size_t slot = 8 * (size_t)K * NT;
   const size_t budget = 160 * 1024 - 2048;  // headroom below the 160 KiB of a CU (launches at 163808 B fail)
@@ -386,6 +388,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   double* gct = PE ? (double*)(smem + lay.gct) : nullptr;  // [2][NT] continuation entry
   int* peLr = PE ? (int*)(smem + lay.pei) : nullptr;       // [KMAX] rows valid per regime
   int* peEx = PE ? peLr + HYG_KMAX : nullptr;              // [KMAX] exited at the last row
+  int8_t* rpu = PE ? (int8_t*)(smem + lay.rpu) : nullptr;  // [2][NT] r if d >= u else -1
   SgPeChain pc{};
   constexpr int dim = K * K, jw = K * (K - 1);
   const int every = PE ? pe.c.every : 1;
@@ -436,6 +439,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       sg_pe_parts(pc, peLr, peEx, u, my_st, my_base, my_cont, gf, gcn, ov);
       gfr[tid] = gf;
       gct[tid] = gcn;
+      rpu[tid] = (int8_t)(sg_d(my_st) >= u ? sg_r(my_st) : -1);
     }
   } else {
     if (tid < K) sg_trans_parts(md, u, my_st, my_base, my_cont);
@@ -750,50 +754,60 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         // fresh particle (1, q), coordinate j: the sum over the previous
         // particles in kCh fixed chunks of rows (hyg_sgpe_fresh_chunks), each
         // in n order, one (chunk, q, j) task per thread. The gradient of
-        // log f((1, q) | (d_n, r_n)) at j is nonzero only when q != r_n and
-        // d_n >= u, and then it is gomg_n if j is the omega entry of r_n
-        // (r_n == rw), or the constant -P[rb][jj] (+1 if jj == q) if j lies in
-        // the P block of r_n (r_n == rb): branch-free selects over kFb previous
-        // particles loaded at once (phi rows up to 256 exist; the ones >= Np
-        // are not used). Chunk sums meet in LDS (scr) and are added left to right.
+        // log f((1, q) | (d_n, r_n)) at j is nonzero only when q != r_n,
+        // d_n >= u and r_n is j's regime rt (the regime of the omega entry or
+        // of the P block j lies in): then it is gomg_n, resp. the constant
+        // -P[rt][jj] (+1 if jj == q). Per term: one byte compare against
+        // rpu[n] (r_n if d_n >= u, else -1) and a select, over batches of kFb
+        // previous particles loaded at once (phi rows up to 256 exist; the
+        // ones >= Np are not used). Chunk sums meet in LDS (scr) and are added
+        // left to right.
         constexpr int kCh = (K <= 8 ? 512 : 256) / (K * K * K) >= 8 ? 8
                           : (K <= 8 ? 512 : 256) / (K * K * K) >= 4 ? 4
                           : (K <= 8 ? 512 : 256) / (K * K * K) >= 2 ? 2 : 1;
         constexpr int kRows = NT / kCh;
         constexpr int kFb = 8;
         double* part = (double*)(smem + lay.scr);  // [kCh][K][dim] when kCh > 1
+        const int8_t* rpuP = rpu + pb * NT;
         for (int e = tid; e < kCh * K * dim; e += NB) {
           const int ck = e / (K * dim), pq = e - ck * (K * dim);
           const int q = pq / dim, j = pq - q * dim;
-          const int rb = (j < jw) ? j / (K - 1) : -1;
-          const int rw = (j >= jw) ? j - jw : -1;
+          const bool isw = j >= jw;
+          const int rt = isw ? j - jw : j / (K - 1);
           double cval = 0.0;
-          if (rb >= 0) {
-            const int ii = j - rb * (K - 1), jj = (ii < rb) ? ii : ii + 1;
-            cval = -pm->P[rb * K + jj];
+          if (!isw) {
+            const int ii = j - rt * (K - 1), jj = (ii < rt) ? ii : ii + 1;
+            cval = -pm->P[rt * K + jj];
             if (jj == q) cval = cval + 1.0;
           }
+          const int rsel = (rt == q) ? -2 : rt;  // -2 matches no particle
           const double* col = phiP + j;
           const double* bkq = BK + q * NT;
           const int nb0 = ck * kRows, nb1 = (nb0 + kRows < Np) ? nb0 + kRows : Np;
           double acc = 0.0;
           for (int n0 = nb0; n0 < nb1; n0 += kFb) {
             double v[kFb], bk[kFb], gf[kFb];
-            uint32_t sn[kFb];
+            int rp[kFb];
 #pragma unroll
             for (int i = 0; i < kFb; ++i) {
               v[i] = col[(size_t)(n0 + i) * dim];
-              sn[i] = stPP[n0 + i];
+              rp[i] = rpuP[n0 + i];
               bk[i] = bkq[n0 + i];
-              gf[i] = gfrP[n0 + i];
+              gf[i] = isw ? gfrP[n0 + i] : cval;
             }
+            if (n0 + kFb <= nb1) {
 #pragma unroll
-            for (int i = 0; i < kFb; ++i) {
-              const int rp = sg_r(sn[i]);
-              const bool valid = (q != rp) && (sg_d(sn[i]) >= u);
-              const double g = valid ? ((rp == rw) ? gf[i] : ((rp == rb) ? cval : 0.0)) : 0.0;
-              const double term = bk[i] * (v[i] + g);
-              acc = (n0 + i < nb1) ? acc + term : acc;
+              for (int i = 0; i < kFb; ++i) {
+                const double g = (rp[i] == rsel) ? gf[i] : 0.0;
+                acc = acc + bk[i] * (v[i] + g);
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < kFb; ++i) {
+                const double g = (rp[i] == rsel) ? gf[i] : 0.0;
+                const double term = bk[i] * (v[i] + g);
+                acc = (n0 + i < nb1) ? acc + term : acc;
+              }
             }
           }
           if (kCh == 1) phiC[(size_t)(M + q) * dim + j] = acc;
@@ -856,6 +870,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           sg_pe_parts(pc, peLr, peEx, u, my_st, my_base, my_cont, gf, gcn, ov);
           gfr[cb * NT + tid] = gf;
           gct[cb * NT + tid] = gcn;
+          rpu[cb * NT + tid] = (int8_t)(sg_d(my_st) >= u ? sg_r(my_st) : -1);
         }
         if (__syncthreads_or(ov)) {
           status = HYG_ENOMEM;
