@@ -196,7 +196,7 @@ def load() -> C.CDLL:
     L.hyg_sg_run_chains_pe.argtypes = [vp, C.POINTER(SgPeParams), C.POINTER(SgChain), i32, vp, vp, sz, i32, vp, vp,
                                        vp, vp]
     L.hyg_pre_collapse.restype = C.c_int
-    L.hyg_pre_collapse.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, vp, vp]
+    L.hyg_pre_collapse.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i64, i32, vp, vp, i32, i32, vp, vp]
     L.hyg_bed_labels.restype = C.c_int
     L.hyg_bed_labels.argtypes = [vp, i32, i64, vp, vp, vp]
     L.hyg_bed_format.restype = i64

@@ -21,8 +21,8 @@ namespace hyg {
 int bed_launch_labels(const double* probs, int K, int64_t n, int8_t* label, double* score, void* stream);
 int pre_launch_collapse(const int64_t* pos0, int64_t T, const int64_t* plus_start, const int64_t* plus_end,
                         const double* plus_cov, const double* plus_pct, int64_t n_plus, const int64_t* minus_start,
-                        const double* minus_cov, const double* minus_pct, int64_t n_minus, uint8_t* matched,
-                        double* out, int stride, int col, int* conflicts, void* stream);
+                        const double* minus_cov, const double* minus_pct, int64_t n_minus, int single_base,
+                        uint8_t* matched, double* out, int stride, int col, int* conflicts, void* stream);
 }
 
 using namespace hyg;
@@ -726,16 +726,18 @@ int64_t hyg_bed_format(const char* chrom, const int64_t* pos, const int8_t* labe
 
 int hyg_pre_collapse(const int64_t* pos0, int64_t T, const int64_t* plus_start, const int64_t* plus_end,
                      const double* plus_cov, const double* plus_pct, int64_t n_plus, const int64_t* minus_start,
-                     const double* minus_cov, const double* minus_pct, int64_t n_minus, uint8_t* scratch,
-                     double* counts, int32_t stride, int32_t column, int32_t* conflicts, void* stream) {
+                     const double* minus_cov, const double* minus_pct, int64_t n_minus, int32_t plus_single_base,
+                     uint8_t* scratch, double* counts, int32_t stride, int32_t column, int32_t* conflicts,
+                     void* stream) {
   if (T < 0 || n_plus < 0 || n_minus < 0 || stride < 2 || column < 0 || column + 2 > stride)
     return fail(HYG_EINVAL, "invalid sizes (need 0 <= column, column + 2 <= stride)");
   if ((T > 0 && (!pos0 || !counts || !conflicts)) || (n_plus > 0 && (!plus_start || !plus_end || !plus_cov || !plus_pct)) ||
-      (n_minus > 0 && (!minus_start || !minus_cov || !minus_pct || !scratch)))
+      (n_minus > 0 && (!minus_start || !minus_cov || !minus_pct || (!scratch && !plus_single_base))))
     return fail(HYG_EINVAL, "null buffer");
   if (!have_device()) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
   const int rc = pre_launch_collapse(pos0, T, plus_start, plus_end, plus_cov, plus_pct, n_plus, minus_start, minus_cov,
-                                     minus_pct, n_minus, scratch, counts, stride, column, conflicts, stream);
+                                     minus_pct, n_minus, plus_single_base ? 1 : 0, scratch, counts, stride, column,
+                                     conflicts, stream);
   if (rc != HYG_OK) return fail(rc, "preprocess launch failed");
   return HYG_OK;
 }

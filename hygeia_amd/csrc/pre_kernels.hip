@@ -81,7 +81,7 @@ pre_grid_kernel(const int64_t* __restrict__ pos0, int64_t T, const int64_t* __re
                 const int64_t* __restrict__ plus_end, const double* __restrict__ plus_cov,
                 const double* __restrict__ plus_pct, int64_t n_plus, const int64_t* __restrict__ minus_start,
                 const double* __restrict__ minus_cov, const double* __restrict__ minus_pct, int64_t n_minus,
-                const uint8_t* __restrict__ matched, double* __restrict__ out, int stride, int col,
+                const uint8_t* __restrict__ matched, int single_base, double* __restrict__ out, int stride, int col,
                 int* __restrict__ conflicts) {
   constexpr int kWin = 1024;
   __shared__ int64_t win[4];  // plus [lo, hi), minus [lo, hi) of the chunk
@@ -125,7 +125,8 @@ pre_grid_kernel(const int64_t* __restrict__ pos0, int64_t T, const int64_t* __re
     } else {
       jm = pre_find_in(minus_start, win[2], win[3], k + 1);
     }
-    const bool minus_only = jm >= 0 && !matched[jm];
+    // single-base "+" records: the only "+" record ending at k + 1 starts at k
+    const bool minus_only = jm >= 0 && (single_base ? ip < 0 : !matched[jm]);
     double cp = 0.0, pp = 0.0, cn = 0.0, pn = 0.0;
     bool have = false;
     if (ip >= 0) {
@@ -166,21 +167,21 @@ pre_grid_kernel(const int64_t* __restrict__ pos0, int64_t T, const int64_t* __re
 
 int pre_launch_collapse(const int64_t* pos0, int64_t T, const int64_t* plus_start, const int64_t* plus_end,
                         const double* plus_cov, const double* plus_pct, int64_t n_plus, const int64_t* minus_start,
-                        const double* minus_cov, const double* minus_pct, int64_t n_minus, uint8_t* matched,
-                        double* out, int stride, int col, int* conflicts, void* stream) {
+                        const double* minus_cov, const double* minus_pct, int64_t n_minus, int single_base,
+                        uint8_t* matched, double* out, int stride, int col, int* conflicts, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (n_minus > 0 && hipMemsetAsync(matched, 0, (size_t)n_minus, s) != hipSuccess) return HYG_EDEVICE;
+  if (!single_base && n_minus > 0 && hipMemsetAsync(matched, 0, (size_t)n_minus, s) != hipSuccess) return HYG_EDEVICE;
   auto grid = [](int64_t n) {
     int64_t b = (n + 255) / 256;
     return (unsigned)(b < 1 ? 1 : (b > 256 * 32 ? 256 * 32 : b));
   };
-  if (n_plus > 0 && n_minus > 0)
+  if (!single_base && n_plus > 0 && n_minus > 0)
     hipLaunchKernelGGL(pre_mark_kernel, dim3(grid(n_plus)), dim3(256), 0, s, plus_end, n_plus, minus_start, n_minus,
                        matched);
   if (T > 0)
     hipLaunchKernelGGL(pre_grid_kernel, dim3(grid(T)), dim3(256), 0, s, pos0, T, plus_start, plus_end, plus_cov,
-                       plus_pct, n_plus, minus_start, minus_cov, minus_pct, n_minus, matched, out, stride, col,
-                       conflicts);
+                       plus_pct, n_plus, minus_start, minus_cov, minus_pct, n_minus, matched, single_base, out, stride,
+                       col, conflicts);
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }
 

@@ -10,7 +10,7 @@ n_total_reads_{control,case}}_{chromosome}.txt.gz`, np.savetxt fmt '%s',
 The text is parsed on the host (pandas; the reference uses polars 1.8.2,
 absent here); the strand collapse and the counts on the CpG grid run on the
 device (hyg_pre_collapse, hygeia_amd/csrc/pre_kernels.hip), one sample at a
-time into a [sites][2 samples] matrix in HBM. Reference behaviours kept:
+time into its own [sites][2] block in HBM. Reference behaviours kept:
 * sites of a sample that are not CpG sites of the CpG file are dropped (the
   full joins give them a null Pos0, :365-369), CpG sites a sample lacks are 0
   (np.nan_to_num, :384); a missing sample file gives 0 columns (:281-287);
@@ -84,8 +84,8 @@ def read_bed(path: str, chromosome: str):
     return out, len(df)
 
 
-def collapse_on_device(pos0_dev, strands, counts_dev, column: int, stream) -> None:
-    """hyg_pre_collapse for one sample into counts[:, column:column + 2]."""
+def collapse_on_device(pos0_dev, strands, counts_dev, stream) -> None:
+    """hyg_pre_collapse for one sample into its contiguous counts block [sites][2]."""
     import torch
 
     L = _lib.load()
@@ -93,12 +93,13 @@ def collapse_on_device(pos0_dev, strands, counts_dev, column: int, stream) -> No
     (ps, pe, pc, pp), (ms, _me, mc, mp) = strands
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     d = [t(x) for x in (ps, pe, pc, pp, ms, mc, mp)]
+    single = int(bool(np.all(pe == ps + 1)))  # single-base "+" records: no marking pass
     scratch = torch.empty(max(len(ms), 1), dtype=torch.uint8, device=dev)
     conflicts = torch.zeros(1, dtype=torch.int32, device=dev)
     _lib.check(L.hyg_pre_collapse(pos0_dev.data_ptr(), pos0_dev.numel(), d[0].data_ptr(), d[1].data_ptr(),
                                   d[2].data_ptr(), d[3].data_ptr(), len(ps), d[4].data_ptr(), d[5].data_ptr(),
-                                  d[6].data_ptr(), len(ms), scratch.data_ptr(), counts_dev.data_ptr(),
-                                  counts_dev.shape[1], column, conflicts.data_ptr(), stream))
+                                  d[6].data_ptr(), len(ms), single, scratch.data_ptr(), counts_dev.data_ptr(), 2, 0,
+                                  conflicts.data_ptr(), stream))
     if int(conflicts.item()) != 0:
         raise ValueError(f"{int(conflicts.item())} CpG sites claimed by two collapsed rows (records longer "
                          "than one base are not supported)")
@@ -120,7 +121,7 @@ def process(cpg_file_path: str, output_path: str, chromosome: str, case_paths: L
     samples = [(p, i) for p, i in zip(control_paths, control_ids)] + [(p, i) for p, i in zip(case_paths, case_ids)]
     T = pos0.size
     pos0_dev = torch.from_numpy(pos0).to(dev)
-    counts = torch.full((T, 2 * len(samples)), float("nan"), dtype=torch.float64, device=dev)
+    counts = torch.full((len(samples), T, 2), float("nan"), dtype=torch.float64, device=dev)  # per sample [T][2]
     for s, (path, sid) in enumerate(samples):
         logger.info(f"Processing sample: {sid}")
         if not Path(path).exists():
@@ -130,8 +131,8 @@ def process(cpg_file_path: str, output_path: str, chromosome: str, case_paths: L
         if n_rows == 0:
             logger.warning(f"No CpG data found for {sid} on chromosome {chromosome}")
             continue
-        collapse_on_device(pos0_dev, strands, counts, 2 * s, stream)
-    data = counts.cpu().numpy()
+        collapse_on_device(pos0_dev, strands, counts[s], stream)
+    data = counts.permute(1, 0, 2).reshape(T, 2 * len(samples)).cpu().numpy()  # [T][(meth, unmeth) per sample]
     has_null = bool(np.isnan(data).any())
     data = np.nan_to_num(data, copy=False)
     if not has_null:  # polars hands out an Int64 matrix when no value is null

@@ -342,14 +342,17 @@ int64_t hyg_bed_format(const char* chrom, const int64_t* positions, const int8_t
  * round(total (100 - avg) / 100), half away from zero as polars; sites without
  * a collapsed row NaN, the reference's null). Device pointers; each strand's records sorted by start
  * with unique starts (the caller checks); coverage and percent as f64.
- * Writes counts[t * stride + column] = meth, [.. + 1] = unmeth for every site;
- * scratch [n_minus] bytes; *conflicts (device int, caller-zeroed) counts sites
+ * Writes counts[t * stride + column] = meth, [.. + 1] = unmeth for every site
+ * (stride 2: one sample's contiguous [n_sites][2] block, the fastest layout);
+ * plus_single_base != 0 promises end = start + 1 for every "+" record (the
+ * pairing then needs no marking pass and no scratch); else scratch [n_minus]
+ * bytes; *conflicts (device int, caller-zeroed) counts sites
  * that two collapsed rows claim (records longer than one base). */
 int hyg_pre_collapse(const int64_t* cpg_pos0, int64_t n_sites, const int64_t* plus_start, const int64_t* plus_end,
                      const double* plus_coverage, const double* plus_percent, int64_t n_plus,
                      const int64_t* minus_start, const double* minus_coverage, const double* minus_percent,
-                     int64_t n_minus, uint8_t* scratch, double* counts, int32_t stride, int32_t column,
-                     int32_t* conflicts, void* stream);
+                     int64_t n_minus, int32_t plus_single_base, uint8_t* scratch, double* counts, int32_t stride,
+                     int32_t column, int32_t* conflicts, void* stream);
 
 /* Number of visible HIP devices (0 when none: compute calls then fail). */
 int hyg_device_count(void);

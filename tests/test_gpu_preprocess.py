@@ -108,3 +108,37 @@ def test_preprocess_end_to_end(lib, tmp_path, full):
         assert read_out(tmp_path / "out" / f"{name}_{chrom}.txt.gz") == read_out(tmp_path / f"exp_{name}.txt.gz"), name
     txt = read_out(tmp_path / "out" / f"n_total_reads_case_{chrom}.txt.gz")
     assert (".0" in txt) == (not full)
+
+
+def test_marking_pass_equals_single_base_path(lib):
+    """hyg_pre_collapse with plus_single_base = 0 (the pre_mark_kernel pass)
+    and = 1 (pairing through the grid's own lookup) agree on single-base data."""
+    from hygeia_amd import _lib
+    from hygeia_amd.preprocess import read_bed
+    import ctypes as C
+
+    cpg1, beds = synth(5000, 11)
+    dev = torch.device("cuda", 0)
+    pos0 = torch.from_numpy(np.sort(cpg1 - 1)).to(dev)
+    import tempfile, os
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "s.bed")
+        with open(p, "w") as fh:
+            fh.write("h\n")
+            beds[0].to_csv(fh, sep="\t", index=False, header=False)
+        (ps, pe, pc, pp), (ms, _, mc, mp) = read_bed(p, "22")[0]
+    t = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (ps, pe, pc, pp, ms, mc, mp)]
+    outs = []
+    for single in (0, 1):
+        out = torch.full((pos0.numel(), 2), -7.0, dtype=torch.float64, device=dev)
+        scratch = torch.empty(max(len(ms), 1), dtype=torch.uint8, device=dev)
+        conf = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(lib.hyg_pre_collapse(pos0.data_ptr(), pos0.numel(), t[0].data_ptr(), t[1].data_ptr(),
+                                        t[2].data_ptr(), t[3].data_ptr(), len(ps), t[4].data_ptr(), t[5].data_ptr(),
+                                        t[6].data_ptr(), len(ms), single, scratch.data_ptr(), out.data_ptr(), 2, 0,
+                                        conf.data_ptr(), None))
+        torch.cuda.synchronize()
+        assert int(conf.item()) == 0
+        outs.append(out.cpu().numpy())
+    np.testing.assert_array_equal(np.nan_to_num(outs[0], nan=-1), np.nan_to_num(outs[1], nan=-1))
+    assert np.isfinite(outs[0]).any() and np.isnan(outs[0]).any()

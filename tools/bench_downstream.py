@@ -95,15 +95,15 @@ def main():
     dm = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in minus]
     scratch = torch.empty(minus[0].size, dtype=torch.uint8, device=dev)
     conf = torch.zeros(1, dtype=torch.int32, device=dev)
-    out = torch.empty((T, 2 * S), dtype=torch.float64, device=dev)
+    out = torch.empty((S, T, 2), dtype=torch.float64, device=dev)  # per-sample [T][2] blocks
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def run():
         for s in range(S):  # the same synthetic sample in every column (layout and traffic are what is timed)
             _lib.check(L.hyg_pre_collapse(d_pos.data_ptr(), T, dp[0].data_ptr(), dp[1].data_ptr(), dp[2].data_ptr(),
                                           dp[3].data_ptr(), plus[0].size, dm[0].data_ptr(), dm[1].data_ptr(),
-                                          dm[2].data_ptr(), minus[0].size, scratch.data_ptr(), out.data_ptr(),
-                                          2 * S, 2 * s, conf.data_ptr(), sp))
+                                          dm[2].data_ptr(), minus[0].size, 1, scratch.data_ptr(), out[s].data_ptr(),
+                                          2, 0, conf.data_ptr(), sp))
 
     run()
     torch.cuda.synchronize(dev)
@@ -114,8 +114,8 @@ def main():
     ev1.synchronize()
     ms = ev0.elapsed_time(ev1) / args.reps
     # per sample: pos0 read, the records read once, the match flags written + read, the count pair written
-    bytes_sample = 8 * T + 32 * plus[0].size + 24 * minus[0].size + 2 * minus[0].size + 16 * T
-    chk = out[:, 0:2].cpu().numpy()
+    bytes_sample = 8 * T + 32 * plus[0].size + 24 * minus[0].size + 16 * T  # single-base: no match flags
+    chk = out[0].cpu().numpy()
     n_cpu = min(T, 4_000_000)
     t0 = time.perf_counter()
     ref = cpu_collapse(pos0[:n_cpu], tuple(a[a_ok] for a, a_ok in zip(plus, [plus[0] <= pos0[n_cpu - 1]] * 4)),
@@ -127,7 +127,7 @@ def main():
         "value": T * S / (ms / 1000.0), "unit": "CpG-site-samples/s", "n_gpus": 1, "ms_per_step": ms,
         "dtype": "int64/f64", "data": "synthetic",
         "config": {"workload": f"{T} CpG grid x {S} samples, 75% + / 75% - strand records per sample"},
-        "roofline": {"bound": "hbm", "kernel": "pre_grid_kernel + pre_mark_kernel",
+        "roofline": {"bound": "hbm", "kernel": "pre_grid_kernel",
                      "achieved": bytes_sample * S / (ms / 1000.0) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": bytes_sample * S / (ms / 1000.0) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_unit": bytes_sample / T},
