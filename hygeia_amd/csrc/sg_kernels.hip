@@ -292,7 +292,8 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 // Bitonic sort of the NT (key, idx) pairs held one per thread into descending
 // key, ties by ascending idx (the order of arma::sort_index "descend" /
 // oracle sort_desc); afterwards thread q holds the element of sorted position
-// q. Distances < 64 exchange through lane shuffles, 64 and 128 through LDS
+// q. Distances < 64 exchange within the wave (xshfl: DPP, row rotations,
+// permlane swaps), 64 and 128 through LDS
 // (xk / xi, two buffers so consecutive cross-wave steps need one barrier each).
 template <int NB>
 __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk, int* xi) {
@@ -312,9 +313,15 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
         pk = xk[buf * NB + (tid ^ j)];
         pi = xi[buf * NB + (tid ^ j)];
         buf ^= 1;
-      } else {
-        pk = shfl_xor64(key, j);
-        pi = __shfl_xor(idx, j);
+      } else {  // within a wave: DPP / permlane swaps (no LDS round trip), j constant after unrolling
+        switch (j) {
+          case 1: pk = xshfl64<1>(key); pi = (int)xshfl32<1>((uint32_t)idx); break;
+          case 2: pk = xshfl64<2>(key); pi = (int)xshfl32<2>((uint32_t)idx); break;
+          case 4: pk = xshfl64<4>(key); pi = (int)xshfl32<4>((uint32_t)idx); break;
+          case 8: pk = xshfl64<8>(key); pi = (int)xshfl32<8>((uint32_t)idx); break;
+          case 16: pk = xshfl64<16>(key); pi = (int)xshfl32<16>((uint32_t)idx); break;
+          default: pk = xshfl64<32>(key); pi = (int)xshfl32<32>((uint32_t)idx); break;
+        }
       }
       const bool up = (tid & k) == 0, lower = (tid & j) == 0;
       const bool pfirst = pk > key || (pk == key && pi < idx);
