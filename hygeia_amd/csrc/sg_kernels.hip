@@ -297,23 +297,28 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 // (xk / xi, two buffers so consecutive cross-wave steps need one barrier each).
 template <int NB>
 __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk, int* xi) {
-  constexpr int NT = kSgThreads;  // the keys sorted: threads [0, 256) (threads >= 256 sort their own dummies)
+  constexpr int NT = kSgThreads;  // the keys sorted: threads [0, 256)
   const int tid = threadIdx.x;
+  const bool real = (NB == NT) || tid < NT;  // wave-uniform: waves >= 4 hold no keys and only keep the barriers
   int buf = 0;
 #pragma unroll
   for (int k = 2; k <= NT; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      uint64_t pk;
-      int pi;
+      uint64_t pk = key;
+      int pi = idx;
       if (j >= 64) {
-        xk[buf * NB + tid] = key;
-        xi[buf * NB + tid] = idx;
+        if (real) {
+          xk[buf * NB + tid] = key;
+          xi[buf * NB + tid] = idx;
+        }
         lds_barrier();
-        pk = xk[buf * NB + (tid ^ j)];
-        pi = xi[buf * NB + (tid ^ j)];
+        if (real) {
+          pk = xk[buf * NB + (tid ^ j)];
+          pi = xi[buf * NB + (tid ^ j)];
+        }
         buf ^= 1;
-      } else {  // within a wave: DPP / permlane swaps (no LDS round trip), j constant after unrolling
+      } else if (real) {  // within a wave: DPP / permlane swaps (no LDS round trip), j constant after unrolling
         switch (j) {
           case 1: pk = xshfl64<1>(key); pi = (int)xshfl32<1>((uint32_t)idx); break;
           case 2: pk = xshfl64<2>(key); pi = (int)xshfl32<2>((uint32_t)idx); break;
@@ -323,11 +328,13 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
           default: pk = xshfl64<32>(key); pi = (int)xshfl32<32>((uint32_t)idx); break;
         }
       }
-      const bool up = (tid & k) == 0, lower = (tid & j) == 0;
-      const bool pfirst = pk > key || (pk == key && pi < idx);
-      if ((lower == up) ? pfirst : !pfirst) {
-        key = pk;
-        idx = pi;
+      if (real) {
+        const bool up = (tid & k) == 0, lower = (tid & j) == 0;
+        const bool pfirst = pk > key || (pk == key && pi < idx);
+        if ((lower == up) ? pfirst : !pfirst) {
+          key = pk;
+          idx = pi;
+        }
       }
     }
   }
@@ -653,9 +660,16 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       }
       double* redd = (double*)red;
       hyg_u128* redu = (hyg_u128*)(red + 8 * NW * K);
+      // waves >= 4 of a 512-thread group hold no particle: they write neutral
+      // partials (-inf maxima, zero sums) instead of reducing -inf rows
+      const bool realw = (NB == NT) || wv < NT / 64;
       double mq[K];
 #pragma unroll
-      for (int q = 0; q < K; ++q) mq[q] = wave_max(vb[q]);
+      for (int q = 0; q < K; ++q) mq[q] = HYG_NINF;
+      if (realw) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) mq[q] = wave_max(vb[q]);
+      }
       if (lane == 0) {
 #pragma unroll
         for (int q = 0; q < K; ++q) redd[wv * K + q] = mq[q];
@@ -673,11 +687,18 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         hyg_u128 s2[K];
 #pragma unroll
         for (int q = 0; q < K; ++q) {
-          ev[q] = hyg_exp(vb[q] - mq[q]);
-          s2[q] = hyg_fix100(ev[q]);
+          ev[q] = 0.0;
+          s2[q] = hyg_u128_zero();
         }
+        if (realw) {
 #pragma unroll
-        for (int q = 0; q < K; ++q) s2[q] = wave_sum128(s2[q]);
+          for (int q = 0; q < K; ++q) {
+            ev[q] = hyg_exp(vb[q] - mq[q]);
+            s2[q] = hyg_fix100(ev[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < K; ++q) s2[q] = wave_sum128(s2[q]);
+        }
         if (lane == 0) {
 #pragma unroll
           for (int q = 0; q < K; ++q) redu[wv * K + q] = s2[q];
@@ -717,10 +738,15 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         status = HYG_ENUMERIC;
         break;
       }
-      logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NB>(hyg_fix100(hyg_exp(nlw - mx)), red), 100));
+      {
+        hyg_u128 fx = hyg_u128_zero();
+        if (realw) fx = hyg_fix100(hyg_exp(nlw - mx));
+        logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NB>(fx, red), 100));
+      }
       my_lw = nlw;
       my_st = nst;
-      my_w = (tid < N) ? hyg_exp(nlw - logZ) : 0.0;
+      my_w = 0.0;
+      if (tid < N) my_w = hyg_exp(nlw - logZ);
       if (tid < N) {
         st_[cb * NT + tid] = my_st;
         lw_[cb * NT + tid] = my_lw;
