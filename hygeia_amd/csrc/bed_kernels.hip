@@ -20,8 +20,18 @@ bed_label_kernel(const double* __restrict__ probs, int K, int64_t n, int8_t* __r
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double* row = probs + i * K;
     double v[HYG_KMAX];
+    if ((K & 1) == 0) {  // even K: 16-byte loads (rows are 16-byte aligned)
+      const double2* r2 = (const double2*)row;
 #pragma unroll
-    for (int r = 0; r < HYG_KMAX; ++r) v[r] = (r < K) ? row[r] : 0.0;
+      for (int r = 0; r < HYG_KMAX / 2; ++r) {
+        const double2 x = (2 * r < K) ? r2[r] : make_double2(0.0, 0.0);
+        v[2 * r] = x.x;
+        v[2 * r + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < HYG_KMAX; ++r) v[r] = (r < K) ? row[r] : 0.0;
+    }
     // pmax (NA-free rows): the largest value; the first index attaining it
     double mx = v[0];
     int arg = 0;
