@@ -826,18 +826,18 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
               v[i] = col[(size_t)(n0 + i) * dim];
               rp[i] = rpuP[n0 + i];
               bk[i] = bkq[n0 + i];
-              gf[i] = isw ? gfrP[n0 + i] : cval;
+              gf[i] = gfrP[n0 + i];  // loaded unconditionally, selected below (no exec-mask branches)
             }
             if (n0 + kFb <= nb1) {
 #pragma unroll
               for (int i = 0; i < kFb; ++i) {
-                const double g = (rp[i] == rsel) ? gf[i] : 0.0;
+                const double g = (rp[i] == rsel) ? (isw ? gf[i] : cval) : 0.0;
                 acc = acc + bk[i] * (v[i] + g);
               }
             } else {
 #pragma unroll
               for (int i = 0; i < kFb; ++i) {
-                const double g = (rp[i] == rsel) ? gf[i] : 0.0;
+                const double g = (rp[i] == rsel) ? (isw ? gf[i] : cval) : 0.0;
                 const double term = bk[i] * (v[i] + g);
                 acc = (n0 + i < nb1) ? acc + term : acc;
               }
