@@ -128,7 +128,7 @@ def lib() -> C.CDLL:
         L.oracle_tg_emission.restype = i32
         L.oracle_tg_emission.argtypes = [C.POINTER(TgParams), vp, vp, i32, vp, vp, i32, C.c_int64, vp]
         L.oracle_tg_chain.restype = i32
-        L.oracle_tg_chain.argtypes = [C.POINTER(TgParams), vp, i32, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.oracle_tg_chain.argtypes = [C.POINTER(TgParams), vp, i32, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_tg_trans.restype = d
         L.oracle_tg_trans.argtypes = [C.POINTER(TgParams), i32, u64, u64]
         L.oracle_tg_xi.restype = u64
@@ -185,12 +185,13 @@ def chain(p: TgParams, E: np.ndarray, seed: int, chain_id: int, want_modes: bool
         "split_probs": np.empty(T, np.float32),
         "regime_probs": np.empty((T, 2 * K), np.float32),
         "final_log_weights": np.empty(c.Nmax, np.float64),
+        "final_states": np.empty(c.Nmax, np.uint64),
     }
     modes = np.zeros(T, np.int32)
     logz = C.c_double(0.0)
     rc = lib().oracle_tg_chain(C.byref(p), _ptr(E), T, seed, chain_id, _ptr(out["merged"]), _ptr(out["control"]),
                                _ptr(out["case"]), _ptr(out["split_probs"]), _ptr(out["regime_probs"]),
-                               C.byref(logz), _ptr(out["final_log_weights"]),
+                               C.byref(logz), _ptr(out["final_log_weights"]), _ptr(out["final_states"]),
                                _ptr(modes) if want_modes else None)
     out["status"] = rc
     out["log_z"] = logz.value

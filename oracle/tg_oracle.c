@@ -186,20 +186,59 @@ typedef struct {
   int r_ph; /* t = 0 only */
 } step_rec;
 
+/* Reference-structure variant only: the read counts, evaluated per particle. */
+typedef struct {
+  const uint16_t *meth_c, *tot_c, *meth_k, *tot_k;
+  int s_c, s_k;
+} count_rows;
+
 typedef struct {
   const oracle_model* om;
-  const double* E;
+  const double* E;       /* emission table [T][2K], or NULL with `counts` */
+  const count_rows* counts;
   int T;
   step_rec* rec;
   uint64_t* par_state; /* [T][M] */
   double* par_w;       /* [T][M] */
 } chain_ctx;
 
+/* Sum over samples of BetaBinomial(y | n, alpha_r, beta_r) with the lgamma
+ * terms evaluated on the spot, per particle, as the reference's observation_fn
+ * does (case_control_regime_model.py:197-231); the terms and their order are
+ * those of hyg_bb_tables + oracle_tg_emission, so the value is the table's. */
+static double bb_direct(const hyg_tg_consts* c, int r, const uint16_t* my, const uint16_t* nt, int S) {
+  const double a = c->alpha[r], b = c->beta[r];
+  const double cst = lgamma(a + b) - lgamma(a) - lgamma(b);
+  double e = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const int n = nt[s], y = my[s];
+    if (n == 0) continue;
+    double term = lgamma((double)n + 1.0) - lgamma((double)y + 1.0);
+    term = term - lgamma((double)(n - y) + 1.0);
+    term = term + lgamma((double)y + a);
+    term = term + lgamma((double)(n - y) + b);
+    term = term - lgamma((double)n + a + b);
+    term = term + cst;
+    e = e + term;
+  }
+  return e;
+}
+
+static double log_obs(const chain_ctx* cx, int t, uint64_t x) {
+  const hyg_tg_consts* c = &cx->om->c;
+  if (!cx->counts) {
+    const double* Et = cx->E + (size_t)t * 2 * c->K;
+    return Et[hyg_st_rc(x)] + Et[c->K + hyg_st_rk(x)];
+  }
+  const count_rows* q = cx->counts;
+  return bb_direct(c, hyg_st_rc(x), q->meth_c + (size_t)t * q->s_c, q->tot_c + (size_t)t * q->s_c, q->s_c) +
+         bb_direct(c, hyg_st_rk(x), q->meth_k + (size_t)t * q->s_k, q->tot_k + (size_t)t * q->s_k, q->s_k);
+}
+
 /* particles of step t: st[n], W[n] for n < return value */
 static int gen_particles(const chain_ctx* cx, int t, uint64_t* st, double* W) {
   const hyg_tg_consts* c = &cx->om->c;
   const int K = c->K;
-  const double* Et = cx->E + (size_t)t * 2 * K;
   const step_rec* r = &cx->rec[t];
   if (r->mode == MODE_INIT) {
     /* _filter_first_step: K^2 candidates, prior = transition from the phantom */
@@ -207,7 +246,7 @@ static int gen_particles(const chain_ctx* cx, int t, uint64_t* st, double* W) {
       for (int j = 0; j < K; ++j) {
         const int n = i * K + j;
         st[n] = hyg_st_pack(i == j, 1, i, 1, j);
-        const double obs = Et[i] + Et[K + j];
+        const double obs = log_obs(cx, t, st[n]);
         const double tr = (i == j) ? c->lPc[r->r_ph * K + i] : -INFINITY;
         W[n] = obs + tr;
       }
@@ -223,7 +262,7 @@ static int gen_particles(const chain_ctx* cx, int t, uint64_t* st, double* W) {
       st[n] = x;
       const double tr = tg_trans(cx->om, ps[a], x);
       if (!hyg_isfinite(tr)) { W[n] = -INFINITY; continue; }
-      const double lg = tr + (Et[hyg_st_rc(x)] + Et[K + hyg_st_rk(x)]);
+      const double lg = tr + log_obs(cx, t, x);
       double w;
       if (r->mode == MODE_KEEP) {
         w = pw[a] + lg;
@@ -400,11 +439,12 @@ static int resample_step(chain_ctx* cx, int t, const uint64_t* st, const double*
 /* Whole chain: filter forward over T sites, then backward simulation of B
  * trajectories. E is the emission table [T][2K]. Outputs (host, untrimmed):
  * merged[T][B], control[T][B][2], kase[T][B][2] int16; split[T], regime[T][2K]
- * f32; *log_z; final_w[Nmax] (may be NULL). n_parents_out[T] (may be NULL)
- * receives the number of resampled ancestors of every step (debug). */
+ * f32; *log_z; final_w[Nmax] and the packed final particle states final_st[Nmax]
+ * (either may be NULL; padding entries are -inf / all-ones). mode_out[T] (may be
+ * NULL) receives mode * 65536 + the number of resampled ancestors of every step. */
 int oracle_tg_chain(const hyg_tg_params* p, const double* E, int T, uint64_t seed, uint64_t chain_id,
                     int16_t* merged, int16_t* control, int16_t* kase, float* split, float* regime,
-                    double* log_z, double* final_w, int32_t* mode_out) {
+                    double* log_z, double* final_w, uint64_t* final_st, int32_t* mode_out) {
   if (T < 1 || T >= HYG_DMAX - 2) return HYG_EINVAL;
   oracle_model om;
   int rc = om_init(&om, p, T + 2);
@@ -414,6 +454,7 @@ int oracle_tg_chain(const hyg_tg_params* p, const double* E, int T, uint64_t see
   chain_ctx cx;
   cx.om = &om;
   cx.E = E;
+  cx.counts = NULL;
   cx.T = T;
   cx.rec = (step_rec*)calloc((size_t)T, sizeof(step_rec));
   cx.par_state = (uint64_t*)calloc((size_t)T * M, sizeof(uint64_t));
@@ -451,6 +492,9 @@ int oracle_tg_chain(const hyg_tg_params* p, const double* E, int T, uint64_t see
     *log_z = logS + mx;
     if (final_w) {
       for (int n = 0; n < Nmax; ++n) final_w[n] = (n < N) ? W[n] : -INFINITY;
+    }
+    if (final_st) {
+      for (int n = 0; n < Nmax; ++n) final_st[n] = (n < N) ? st[n] : ~(uint64_t)0;
     }
   }
   /* ---- backward simulation (filter_and_smoother_algorithm.py:368-447).

@@ -1,0 +1,179 @@
+"""GPU parity at the BASELINE.json configurations' own sizes (bit-exact against
+the CPU oracle, every output array compared):
+
+- C5 (configs[4]): 50 + 50 samples, K = 12, M = 50, B = 25 -- the emission on
+  50-sample rows (hyg_tg_emission on the device) and a whole chain;
+- C3 (configs[2]): full-length segment chains of 110 000 sites (the reference's
+  100 000-site segment + 2 x 5 000 buffers, run_inference_two_groups.py:67-72,
+  194-218), 4 + 4 samples, K = 6, M = 50, B = 25: one on the synthetic
+  generative model, and one on a single-regime stretch whose sojourns outgrow
+  the float32 hazard saturation (case_control_regime_model.py:111-168) and wrap
+  the int16 duration outputs (run_inference_two_groups.py:292-314);
+- C2 (configs[1]): one single-group chain of 200 000 sites at the pipeline
+  settings (4 samples, K = 6, N_max = 250, epsilon = 0.01), long enough for the
+  log-weights to reach the large-magnitude regime noted in DESIGN.md 1.
+
+The oracle chains take about a minute each on one core; they run in threads
+(ctypes releases the GIL) started when the module is first used, overlapping
+the GPU work.
+"""
+import concurrent.futures as cf
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+T_LONG = 110_000
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    from hygeia_amd import _lib
+
+    if _lib.load().hyg_device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on an MI355X (gpurun)")
+
+
+def _long_inputs():
+    from hygeia_amd import synthetic as syn
+
+    d = syn.simulate(T_LONG, 4, 4, K=6, seed=41, coverage=100.0)
+    rng = np.random.default_rng(5)
+    tot = rng.poisson(30, size=(T_LONG, 8)).astype(np.uint16)
+    meth = rng.binomial(tot.astype(np.int64), 0.95).astype(np.uint16)
+    c = {"meth_control": meth[:, :4].copy(), "tot_control": tot[:, :4].copy(),
+         "meth_case": meth[:, 4:].copy(), "tot_case": tot[:, 4:].copy()}
+    return {"synthetic": d, "one_regime": c}
+
+
+@pytest.fixture(scope="module")
+def long_refs(oracle):
+    """Oracle runs of the two 110k chains and the 200k single-group chain, in
+    background threads."""
+    from hygeia_amd import synthetic as syn
+    from oracle import sg_binding as sgb
+
+    data = _long_inputs()
+    mu, sg = syn.regime_params(6)
+    p = oracle.make_params(K=6, M=50, B=25, mu=mu, sigma=sg)
+
+    def tg(name):
+        d = data[name]
+        E = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+        return E, oracle.chain(p, E, 2, (7 << 32) | 3)
+
+    sgd = syn.simulate(200_000, 4, 1, K=6, seed=77, coverage=100.0, omega=0.95)
+    psg = sgb.make_params(K=6)
+
+    def sgchain():
+        E = sgb.emission(psg, sgd["meth_control"], sgd["tot_control"])
+        return sgb.chain(psg, E, seed=3, chain_id=5)
+
+    ex = cf.ThreadPoolExecutor(max_workers=3)
+    futs = {"synthetic": ex.submit(tg, "synthetic"), "one_regime": ex.submit(tg, "one_regime"),
+            "sg": ex.submit(sgchain)}
+    yield data, futs, (sgd, psg)
+    ex.shutdown(wait=True)
+
+
+def _compare(res, fw, ex, ref):
+    pr = res.particle
+    np.testing.assert_array_equal(pr["merged_state"], ref["merged"])
+    np.testing.assert_array_equal(pr["control_state"], ref["control"])
+    np.testing.assert_array_equal(pr["case_state"], ref["case"])
+    np.testing.assert_array_equal(ex["split_probs"], ref["split_probs"])
+    np.testing.assert_array_equal(ex["regime_probs"], ref["regime_probs"])
+    assert ex["log_z"] == ref["log_z"]
+    np.testing.assert_array_equal(fw, ref["final_log_weights"])
+
+
+def _model(mu, sg, theta, M, B, max_reads, max_dur):
+    from hygeia_amd import two_group
+
+    return two_group.CaseControlModel(mu, sg, theta, num_resampled_ancestors=M, num_samples_backward=B,
+                                      max_total_reads=max_reads, max_duration=max_dur)
+
+
+@pytest.mark.timeout(300)
+def test_c5_emission_and_chain(oracle):
+    """C5: 50 + 50 samples, K = 12 (N_max = 8400)."""
+    from hygeia_amd import synthetic as syn
+    from hygeia_amd import two_group
+
+    K, M, B, T = 12, 50, 25, 400
+    mu, sg = syn.regime_params(K)
+    d = syn.simulate(T, 50, 50, K=K, seed=3, coverage=100.0)
+    p = oracle.make_params(K=K, M=M, B=B, mu=mu, sigma=sg)
+    theta = np.array(p.theta[: p.theta_len])
+    E_ref = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    maxr = int(max(d["tot_control"].max(), d["tot_case"].max()))
+    model = _model(mu, sg, theta, M, B, maxr, T + 5)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(d[k]).view(np.int16)).to(dev) for k in
+         ("meth_control", "tot_control", "meth_case", "tot_case")}
+    dc = two_group.DeviceChains(model, [(0, T, 4, 99, 0)], T, device=dev, final_weights=True)
+    E = dc.emission(t["meth_control"], t["tot_control"], t["meth_case"], t["tot_case"])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(E.cpu().numpy(), E_ref)
+    ref = oracle.chain(p, E_ref, 4, 99)
+    assert ref["status"] == 0
+    res, fw, ex = two_group.run({"control": d["meth_control"], "case": d["meth_case"]},
+                                {"control": d["tot_control"], "case": d["tot_case"]}, model, 4, 99)
+    _compare(res, fw, ex, ref)
+    # the batched device path gives the same chain
+    dc.run(E)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dc.control.cpu().numpy(), ref["control"])
+    np.testing.assert_array_equal(dc.regime_probs.cpu().numpy(), ref["regime_probs"])
+    assert dc.log_z[0].item() == ref["log_z"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["synthetic", "one_regime"])
+def test_c3_full_length_chain(oracle, long_refs, name):
+    from hygeia_amd import synthetic as syn
+    from hygeia_amd import two_group
+
+    data, futs, _ = long_refs
+    d = data[name]
+    mu, sg = syn.regime_params(6)
+    model = _model(mu, sg, two_group.uniform_theta(6, 0.8), 50, 25,
+                   int(max(d["tot_control"].max(), d["tot_case"].max())), T_LONG)
+    res, fw, ex = two_group.run({"control": d["meth_control"], "case": d["meth_case"]},
+                                {"control": d["tot_control"], "case": d["tot_case"]}, model, 2, (7 << 32) | 3)
+    _, ref = futs[name].result()
+    assert ref["status"] == 0
+    _compare(res, fw, ex, ref)
+    if name == "one_regime":
+        dur = ref["control"][:, :, 0].astype(np.int64)
+        assert dur.min() < 0  # the int16 duration output wrapped (sojourn > 32767 sites)
+
+
+@pytest.mark.timeout(600)
+def test_c2_single_group_200k_chain(long_refs):
+    from hygeia_amd import _lib
+
+    _, futs, (sgd, psg) = long_refs
+    L = _lib.load()
+    p = _lib.SgParams.from_buffer_copy(bytes(psg))
+    h = C.c_void_p()
+    meth = np.ascontiguousarray(sgd["meth_control"], np.uint16)
+    tot = np.ascontiguousarray(sgd["tot_control"], np.uint16)
+    T, S = tot.shape
+    _lib.check(L.hyg_sg_model_create(C.byref(p), int(tot.max()), T + 10, C.byref(h)))
+    try:
+        out = np.full((T, 6), np.nan)
+        rc = L.hyg_sg_run_chain_host(h, meth.ctypes.data_as(C.c_void_p), tot.ctypes.data_as(C.c_void_p), S, T, 3, 5,
+                                     out.ctypes.data_as(C.c_void_p))
+        assert rc == 0, L.hyg_last_error()
+    finally:
+        L.hyg_sg_model_destroy(h)
+    ref = futs["sg"].result()
+    assert ref["status"] == 0
+    bad = np.argwhere(out != ref["regime_probs"])
+    assert bad.size == 0, (len(bad), bad[:5])
+    np.testing.assert_allclose(out.sum(1), 1.0, atol=1e-8)

@@ -1,0 +1,105 @@
+"""GPU: the tiny chains of tests/test_tg_exact.py through the HIP path.
+
+Each configuration runs many seeds as chains of ONE batched launch
+(hyg_tg_run_chains through two_group.DeviceChains) and is compared
+(1) bit for bit with the CPU oracle, chain by chain, and
+(2) with the exact enumeration of the model (tests/tg_exact_model.py): in the
+    keep-all regime the GPU's log Z equals the exact log marginal likelihood
+    given the phantom regime to 1e-12; with M = 2-3 (optimal finite-state
+    resampling active) the seed average of Z_hat / Z stays 1 within its
+    standard error.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_tg_exact import KEEP_ALL_CASES, KEEP_ALL_M, RESAMPLING_CASES, _problem  # noqa: E402
+from tg_exact_model import phantom_regime  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    from hygeia_amd import _lib
+
+    if _lib.load().hyg_device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on an MI355X (gpurun)")
+
+
+def _run_seeds(p, E, K, M, B, seeds, cid):
+    """All seeds as chains of one launch over the same sites."""
+    from hygeia_amd import two_group
+
+    T = E.shape[0]
+    dev = torch.device("cuda", 0)
+    mu = [p.mu[i] for i in range(K)]
+    sg = [p.sigma[i] for i in range(K)]
+    theta = [p.theta[i] for i in range(p.theta_len)]
+    model = two_group.CaseControlModel(mu, sg, theta, minimum_duration=p.minimum_duration,
+                                       num_resampled_ancestors=M, num_samples_backward=B, max_total_reads=64,
+                                       max_duration=T + 5)
+    chains = [(0, T, s, cid, i * T) for i, s in enumerate(seeds)]
+    dc = two_group.DeviceChains(model, chains, T * len(seeds), device=dev, final_weights=True)
+    Ed = torch.from_numpy(np.ascontiguousarray(E)).to(dev)
+    dc.run(Ed)
+    torch.cuda.synchronize()
+    assert (dc.status.cpu().numpy() == 0).all()
+    return dc
+
+
+def _check_chain_bits(oracle, p, E, dc, i, seed, cid, T):
+    ref = oracle.chain(p, E, seed, cid)
+    o = i * T
+    np.testing.assert_array_equal(dc.merged[o:o + T].cpu().numpy(), ref["merged"])
+    np.testing.assert_array_equal(dc.control[o:o + T].cpu().numpy(), ref["control"])
+    np.testing.assert_array_equal(dc.case[o:o + T].cpu().numpy(), ref["case"])
+    np.testing.assert_array_equal(dc.split_probs[o:o + T].cpu().numpy(), ref["split_probs"])
+    np.testing.assert_array_equal(dc.regime_probs[o:o + T].cpu().numpy(), ref["regime_probs"])
+    assert dc.log_z[i].item() == ref["log_z"]
+    np.testing.assert_array_equal(dc.final_w[i].cpu().numpy(), ref["final_log_weights"])
+
+
+@pytest.mark.parametrize("K,T,dseed", KEEP_ALL_CASES)
+def test_keep_all_gpu_vs_oracle_and_exact(oracle, K, T, dseed):
+    B = 8
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=KEEP_ALL_M, B=B)
+    seeds = list(range(24))
+    cid = 40
+    dc = _run_seeds(p, E, K, KEEP_ALL_M, B, seeds, cid)
+    lz = dc.log_z.cpu().numpy()
+    exact = {}
+    for i, s in enumerate(seeds):
+        _check_chain_bits(oracle, p, E, dc, i, s, cid, T)
+        r_ph = phantom_regime(oracle, s, cid, K)
+        if r_ph not in exact:
+            exact[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+        assert abs(lz[i] - exact[r_ph]) < 1e-12 * max(1.0, abs(exact[r_ph]))
+    assert len(exact) >= 2
+
+
+@pytest.mark.parametrize("K,T,M,dseed", RESAMPLING_CASES)
+def test_resampling_gpu_vs_oracle_and_unbiased_z(oracle, K, T, M, dseed):
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2)
+    seeds = list(range(8192))
+    cid = 3
+    dc = _run_seeds(p, E, K, M, 2, seeds, cid)
+    for i in range(0, len(seeds), 511):  # bit-exact spot checks across the batch
+        _check_chain_bits(oracle, p, E, dc, i, seeds[i], cid, T)
+    lz = dc.log_z.cpu().numpy()
+    zex = {}
+    ratios = []
+    for i, s in enumerate(seeds):
+        r_ph = phantom_regime(oracle, s, cid, K)
+        if r_ph not in zex:
+            zex[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+        ratios.append(math.exp(lz[i] - zex[r_ph]))
+    r = np.array(ratios)
+    se = r.std() / math.sqrt(len(r))
+    assert abs(r.mean() - 1.0) < 4 * se + 1e-3, (r.mean(), se)

@@ -1,0 +1,184 @@
+"""The two-group oracle against an EXACT enumeration of the model (CPU only).
+
+The reference ships no fixtures and TF 2.3 cannot run here, so
+the chain is pinned by an independent numpy/scipy restatement of the model
+(tests/tg_exact_model.py) on tiny chains whose state space can be enumerated:
+
+(i)   keep-all regime (M large: filter_and_smoother_algorithm.py:207-209 at every
+      step): the particle filter enumerates every path, so the oracle's log Z
+      must equal the exact log marginal likelihood given the phantom regime,
+      and its normalised final weights, pooled by state, the exact filter
+      marginal -- both to 1e-12;
+(ii)  the backward simulation (filter_and_smoother_algorithm.py:368-447) draws
+      i.i.d. from the exact smoothing distribution in that regime: chi-square
+      tests of the per-site state marginals and of the (t, t+1) pair marginals
+      pooled over seeds;
+(iii) with M = 2-3 the optimal finite-state resampling (resampling_functions.py:
+      7-52, systematic :56-69) and the weight correction -min(0, log c + W -
+      lse) (filter_and_smoother_algorithm.py:238-270) are active; the estimate
+      Z_hat must stay unbiased: the seed average of Z_hat / Z(r_ph) is 1 within
+      its standard error.
+"""
+import math
+import os
+import sys
+from collections import Counter
+
+import numpy as np
+import pytest
+from scipy import stats
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from tg_exact_model import ExactModel, phantom_regime, unpack  # noqa: E402
+
+MODE_KEEP, MODE_OPTIMAL, MODE_UNBIASED = 0, 1, 2
+KEEP_ALL_M = 64  # above the largest finite particle count of these chains (53)
+KEEP_ALL_CASES = [(2, 5, 1), (3, 4, 2), (3, 3, 3), (2, 6, 4), (2, 1, 5), (3, 2, 6)]
+RESAMPLING_CASES = [(3, 8, 3, 24), (3, 5, 3, 22), (2, 7, 2, 23)]
+
+
+def _problem(oracle, K, T, seed, M, B, cov=12, p_random=True):
+    rng = np.random.default_rng(seed)
+    mu = [(i + 0.5) / K for i in range(K)]
+    sg = [0.08 + 0.04 * (i % 2) for i in range(K)]
+    if p_random:  # a non-uniform control transition matrix and omegas
+        P = rng.dirichlet(np.ones(K - 1) * 2.0, size=K)
+        Pm = np.zeros((K, K))
+        for r in range(K):
+            Pm[r, [c for c in range(K) if c != r]] = P[r]
+        om = rng.uniform(0.6, 0.9, size=K)
+        theta = oracle.theta_from(Pm, om)
+    else:
+        theta = None
+    p = oracle.make_params(K=K, M=M, B=B, mu=mu, sigma=sg, theta=theta, u=2)
+    theta = np.array(p.theta[: p.theta_len])
+    tot = rng.poisson(cov, size=(T, 2)).astype(np.uint16)
+    # methylation levels drawn from the regimes, with a change in the case group
+    lev = np.where(np.arange(T)[:, None] < T // 2, 0.2, 0.8) * np.array([[1.0, 0.5]]) + np.array([[0.1, 0.3]])
+    meth = rng.binomial(tot.astype(np.int64), np.clip(lev, 0.01, 0.99)).astype(np.uint16)
+    d = {"meth_control": meth[:, :1].copy(), "tot_control": tot[:, :1].copy(),
+         "meth_case": meth[:, 1:].copy(), "tot_case": tot[:, 1:].copy()}
+    ex = ExactModel(K, mu, sg, theta, u=2)
+    E = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    E_ex = ex.emission(d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    return p, ex, E, E_ex
+
+
+@pytest.mark.parametrize("K,T,dseed", [(2, 5, 1), (3, 4, 2), (3, 3, 3), (2, 6, 4)])
+def test_emission_matches_scipy(oracle, K, T, dseed):
+    _, _, E, E_ex = _problem(oracle, K, T, dseed, M=10, B=5)
+    np.testing.assert_allclose(E, E_ex, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("K,T,dseed", KEEP_ALL_CASES)
+def test_keep_all_log_z_and_filter_marginal(oracle, K, T, dseed):
+    M = KEEP_ALL_M
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=4)
+    seen = set()
+    for seed in range(12):
+        cid = 40 + seed
+        out = oracle.chain(p, E, seed, cid, want_modes=True)
+        assert out["status"] == 0
+        assert np.all(out["modes"][1:] // 65536 == MODE_KEEP), "M too small for the keep-all regime"
+        r_ph = phantom_regime(oracle, seed, cid, K)
+        seen.add(r_ph)
+        log_z, alphas, _, _ = ex.forward_backward(E_ex, r_ph)
+        assert abs(out["log_z"] - log_z) < 1e-12 * max(1.0, abs(log_z)), (out["log_z"], log_z)
+        # final weights pooled by state = exact filter marginal
+        w, st = out["final_log_weights"], out["final_states"]
+        fin = np.isfinite(w)
+        pooled = Counter()
+        for s, lw in zip(st[fin], w[fin]):
+            pooled[unpack(s)] += math.exp(lw - out["log_z"])
+        exact = {x: math.exp(a - log_z) for x, a in alphas[-1].items()}
+        assert set(pooled) == set(exact)
+        for x in exact:
+            assert abs(pooled[x] - exact[x]) < 1e-12, (x, pooled[x], exact[x])
+    assert len(seen) >= 2  # the phantom regime varies over seeds
+
+
+def _chi2_pvalue(counts: Counter, probs: dict, n: int) -> float:
+    """Pearson chi-square of observed counts against exact probabilities, bins
+    with expectation < 5 pooled."""
+    obs, exp, o_rest, e_rest = [], [], 0, 0.0
+    for k, pk in probs.items():
+        e = n * pk
+        if e >= 5:
+            obs.append(counts.get(k, 0))
+            exp.append(e)
+        else:
+            o_rest += counts.get(k, 0)
+            e_rest += e
+    assert sum(counts.values()) == n
+    assert all(k in probs for k in counts), "a drawn state has probability 0"
+    if e_rest >= 5:
+        obs.append(o_rest)
+        exp.append(e_rest)
+    if len(obs) < 2:
+        return None
+    obs, exp = np.array(obs, float), np.array(exp)
+    exp *= obs.sum() / exp.sum()
+    return float(stats.chisquare(obs, exp).pvalue)
+
+
+@pytest.mark.parametrize("K,T,dseed", [(2, 5, 11), (3, 4, 12)])
+def test_backward_draws_follow_exact_smoother(oracle, K, T, dseed):
+    M, B, nseeds = KEEP_ALL_M, 60, 300
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=B, cov=2)  # weak data: a spread-out posterior
+    # per phantom regime: exact smoother, and pooled draws
+    exact = {}
+    draws = {}
+    for seed in range(nseeds):
+        cid = 7
+        r_ph = phantom_regime(oracle, seed, cid, K)
+        if r_ph not in exact:
+            exact[r_ph] = ex.forward_backward(E_ex, r_ph)
+            draws[r_ph] = [Counter() for _ in range(T)], [Counter() for _ in range(T - 1)]
+        out = oracle.chain(p, E, seed, cid)
+        assert out["status"] == 0
+        m, c, k = out["merged"].astype(int), out["control"].astype(int), out["case"].astype(int)
+        for b in range(B):
+            path = [(m[t, b], c[t, b, 0], c[t, b, 1], k[t, b, 0], k[t, b, 1]) for t in range(T)]
+            for t in range(T):
+                draws[r_ph][0][t][path[t]] += 1
+            for t in range(T - 1):
+                draws[r_ph][1][t][(path[t], path[t + 1])] += 1
+    pvals = []
+    for r_ph, (single, pair) in draws.items():
+        _, _, smooth, pairs = exact[r_ph]
+        n = sum(single[0].values())
+        for t in range(T):
+            pvals.append(_chi2_pvalue(single[t], smooth[t], n))
+        for t in range(T - 1):
+            pvals.append(_chi2_pvalue(pair[t], pairs[t], n))
+    assert len(draws) >= 2
+    pvals = [q for q in pvals if q is not None]
+    assert len(pvals) >= 2 * T  # enough bins with mass to test
+    # deterministic seeds: a fixed set of p-values; each must be unremarkable
+    assert min(pvals) > 1e-4, sorted(pvals)[:5]
+    # and, pooled, they must look uniform (no systematic bias)
+    assert stats.kstest(pvals, "uniform").pvalue > 1e-3
+
+
+@pytest.mark.parametrize("K,T,M,dseed", RESAMPLING_CASES)
+def test_resampling_keeps_z_unbiased(oracle, K, T, M, dseed):
+    nseeds = 20000
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2)
+    zex = {}
+    ratios = []
+    modes = Counter()
+    for seed in range(nseeds):
+        cid = 3
+        r_ph = phantom_regime(oracle, seed, cid, K)
+        if r_ph not in zex:
+            zex[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+        out = oracle.chain(p, E, seed, cid, want_modes=True)
+        assert out["status"] == 0
+        modes.update((out["modes"][1:] // 65536).tolist())
+        ratios.append(math.exp(out["log_z"] - zex[r_ph]))
+    assert modes[MODE_OPTIMAL] > nseeds  # the optimal resampling ran on most steps
+    r = np.array(ratios)
+    se = r.std() / math.sqrt(len(r))
+    assert abs(r.mean() - 1.0) < 4 * se + 1e-3, (r.mean(), se, dict(modes))
+    # the estimate is not degenerate: resampling actually adds variance
+    assert r.std() > 1e-3
