@@ -24,6 +24,19 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp
          "-Wall", "-Wno-unused-function"]
 
 
+def source_hash() -> str:
+    """Digest of every file compiled into the library plus the flags: tags
+    measurements (profiles/pmc_*.json) with the kernel build they were taken on."""
+    import hashlib
+
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for d in sorted(DEPS):
+        h.update(os.path.relpath(d, ROOT).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def stale() -> bool:
     if not os.path.exists(LIB):
         return True

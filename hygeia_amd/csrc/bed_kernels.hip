@@ -14,13 +14,14 @@
 
 namespace hyg {
 
+template <bool VEC>
 __global__ void __launch_bounds__(256)
 bed_label_kernel(const double* __restrict__ probs, int K, int64_t n, int8_t* __restrict__ label,
                  double* __restrict__ score) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double* row = probs + i * K;
     double v[HYG_KMAX];
-    if ((K & 1) == 0) {  // even K: 16-byte loads (rows are 16-byte aligned)
+    if (VEC) {  // even K and a 16-byte aligned base: 16-byte loads
       const double2* r2 = (const double2*)row;
 #pragma unroll
       for (int r = 0; r < HYG_KMAX / 2; ++r) {
@@ -53,8 +54,15 @@ int bed_launch_labels(const double* probs, int K, int64_t n, int8_t* label, doub
   if (n <= 0) return HYG_OK;
   int64_t blocks = (n + 255) / 256;
   if (blocks > 256 * 32) blocks = 256 * 32;
-  hipLaunchKernelGGL(bed_label_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, probs, K, n, label,
-                     score);
+  // the 16-byte row loads need every row 16-byte aligned: K even and the base
+  // aligned (a caller may pass any 8-byte aligned view, e.g. buf[1:])
+  const bool vec = (K & 1) == 0 && ((uintptr_t)probs & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(bed_label_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, probs, K, n,
+                       label, score);
+  else
+    hipLaunchKernelGGL(bed_label_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, probs, K, n,
+                       label, score);
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }
 

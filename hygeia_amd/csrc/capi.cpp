@@ -53,6 +53,53 @@ hipError_t dmalloc_copy(T** dst, const T* src, size_t count) {
   return e;
 }
 
+// The current HIP device must be the one a model's tables live on.
+bool on_model_device(int device) {
+  int cur = -1;
+  return hipGetDevice(&cur) == hipSuccess && cur == device;
+}
+
+// Host-to-device upload of per-launch descriptors through a pinned buffer owned
+// by the model: the async copy reads memory that outlives the call, and the
+// buffer is reused only once the previous upload from it has completed.
+struct PinnedStage {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+
+  hipError_t upload(void* dst, const void* src, size_t n, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    if (pending) {
+      e = hipEventSynchronize(ev);
+      if (e != hipSuccess) return e;
+      pending = false;
+    }
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (n > cap) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+      if ((e = hipHostMalloc(&p, n, hipHostMallocDefault)) != hipSuccess) return e;
+      cap = n;
+    }
+    std::memcpy(p, src, n);
+    if ((e = hipMemcpyAsync(dst, p, n, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
+    pending = true;
+    return hipSuccess;
+  }
+  void release() {
+    if (pending) (void)hipEventSynchronize(ev);
+    if (ev) (void)hipEventDestroy(ev);
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    ev = nullptr;
+    cap = 0;
+    pending = false;
+  }
+};
+
 }  // namespace
 
 struct hyg_tg_model {
@@ -68,6 +115,7 @@ struct hyg_tg_model {
   double* d_lf = nullptr;
   double* d_lg = nullptr;
   double* d_cst = nullptr;
+  mutable PinnedStage stage;  // descriptor uploads (a model is used by one thread at a time)
 
   ModelDev dev() const {
     ModelDev m{};
@@ -91,6 +139,8 @@ struct hyg_sg_model {
   std::vector<double> hz, lf, lg, cst;
   std::vector<uint8_t> ex;
   bool on_device = false;
+  int device = -1;
+  mutable PinnedStage stage;  // descriptor uploads (a model is used by one thread at a time)
   hyg_sg_consts* d_consts = nullptr;
   double* d_hz = nullptr;
   uint8_t* d_ex = nullptr;
@@ -155,6 +205,7 @@ void hyg_tg_params_default(hyg_tg_params* p) {
 void hyg_tg_model_destroy(hyg_tg_model* m) {
   if (!m) return;
   if (m->on_device) {
+    m->stage.release();
     (void)hipFree(m->d_consts);
     (void)hipFree(m->d_hz);
     (void)hipFree(m->d_lf);
@@ -211,6 +262,7 @@ int hyg_tg_emission(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_
                     void* stream) {
   if (!m) return fail(HYG_EINVAL, "null model");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
   if (s_c < 0 || s_k < 0 || n_sites < 0) return fail(HYG_EINVAL, "negative size");
   if (n_sites > 0 && (!E || (s_c && (!meth_c || !tot_c)) || (s_k && (!meth_k || !tot_k))))
     return fail(HYG_EINVAL, "null buffer");
@@ -231,6 +283,7 @@ int hyg_tg_run_chains(const hyg_tg_model* m, const hyg_tg_chain* chains, int32_t
                       void* workspace, size_t workspace_bytes, const hyg_tg_outputs* out, void* stream) {
   if (!m || !chains || !out || !E || !workspace) return fail(HYG_EINVAL, "null argument");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
   if (n_chains <= 0) return HYG_OK;
   if (!out->merged || !out->control || !out->kase || !out->split_probs || !out->regime_probs || !out->log_z)
     return fail(HYG_EINVAL, "null output buffer");
@@ -256,7 +309,7 @@ int hyg_tg_run_chains(const hyg_tg_model* m, const hyg_tg_chain* chains, int32_t
   if (off > workspace_bytes) return fail(HYG_EINVAL, "workspace too small (see hyg_tg_workspace_bytes)");
   uint8_t* ws = (uint8_t*)workspace;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemcpyAsync(ws, cd.data(), sizeof(ChainDev) * n_chains, hipMemcpyHostToDevice, s) != hipSuccess)
+  if (m->stage.upload(ws, cd.data(), sizeof(ChainDev) * n_chains, s) != hipSuccess)
     return fail(HYG_EDEVICE, "descriptor upload failed");
   hyg_tg_outputs o = *out;
   if (!o.status) o.status = (int32_t*)(ws + sizeof(ChainDev) * n_chains);
@@ -272,6 +325,7 @@ int hyg_tg_run_chain_host(const hyg_tg_model* m, const uint16_t* meth_c, const u
                           float* regime, double* log_z, double* final_w) {
   if (!m) return fail(HYG_EINVAL, "null model");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
   if (T < 1) return fail(HYG_EINVAL, "no sites");
   for (int64_t i = 0; i < (int64_t)T * s_c; ++i)
     if (meth_c[i] > tot_c[i] || tot_c[i] > m->nmax_reads) return fail(HYG_EINVAL, "invalid control counts");
@@ -365,6 +419,7 @@ void hyg_sg_params_default(hyg_sg_params* p) {
 void hyg_sg_model_destroy(hyg_sg_model* m) {
   if (!m) return;
   if (m->on_device) {
+    m->stage.release();
     (void)hipFree(m->d_consts);
     (void)hipFree(m->d_hz);
     (void)hipFree(m->d_ex);
@@ -405,6 +460,7 @@ int hyg_sg_model_create(const hyg_sg_params* params, int32_t max_total_reads, in
   m->cst.resize(K);
   hyg_sg_bb_tables(&m->c, max_total_reads, m->lf.data(), m->lg.data(), m->cst.data());
   if (have_device()) {
+    (void)hipGetDevice(&m->device);
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = dmalloc_copy(&m->d_consts, &m->c, 1);
     if (e == hipSuccess) e = dmalloc_copy(&m->d_hz, m->hz.data(), m->hz.size());
@@ -426,6 +482,7 @@ int hyg_sg_emission(const hyg_sg_model* m, const uint16_t* meth, const uint16_t*
                     int64_t n_sites, double* E, void* stream) {
   if (!m) return fail(HYG_EINVAL, "null model");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
   if (n_samples < 0 || n_sites < 0) return fail(HYG_EINVAL, "negative size");
   if (n_sites > 0 && (!E || (n_samples && (!meth || !tot)))) return fail(HYG_EINVAL, "null buffer");
   int rc = sg_launch_emission(m->dev(), m->c, meth, tot, n_samples, n_sites, E, stream);
@@ -449,6 +506,7 @@ int hyg_sg_run_chains(const hyg_sg_model* m, const hyg_sg_chain* chains, int32_t
                       int32_t* status, void* stream) {
   if (!m || !chains || !E || !workspace || !regime_probs) return fail(HYG_EINVAL, "null argument");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
   if (n_chains <= 0) return HYG_OK;
   if (psi_capacity < 0 || psi_capacity > (1 << 24)) return fail(HYG_EINVAL, "psi_capacity out of range");
   const int cap = psi_capacity ? psi_capacity : kSgPsiCapDefault;
@@ -475,7 +533,7 @@ int hyg_sg_run_chains(const hyg_sg_model* m, const hyg_sg_chain* chains, int32_t
   }
   uint8_t* ws = (uint8_t*)workspace;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemcpyAsync(ws, cd.data(), sizeof(SgChainDev) * n_chains, hipMemcpyHostToDevice, s) != hipSuccess)
+  if (m->stage.upload(ws, cd.data(), sizeof(SgChainDev) * n_chains, s) != hipSuccess)
     return fail(HYG_EDEVICE, "descriptor upload failed");
   int32_t* st = status ? status : (int32_t*)(ws + sizeof(SgChainDev) * n_chains);
   int rc = sg_launch_chains(m->dev(), m->c, (const SgChainDev*)ws, n_chains, E, ws, cap, regime_probs, st, stream);
@@ -488,6 +546,7 @@ int hyg_sg_run_chain_host(const hyg_sg_model* m, const uint16_t* meth, const uin
                           uint64_t seed, uint64_t chain_id, double* regime_probs) {
   if (!m || !regime_probs || (S > 0 && (!meth || !tot))) return fail(HYG_EINVAL, "null argument");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
   if (T < 1 || S < 0) return fail(HYG_EINVAL, "no sites");
   for (int64_t i = 0; i < (int64_t)T * S; ++i)
     if (tot[i] > m->nmax_reads) return fail(HYG_EINVAL, "total read count above the model's max_total_reads");
@@ -559,6 +618,7 @@ int hyg_sg_run_chains_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, cons
                          void* stream) {
   if (!m || !pe || !chains || !E || !workspace || !regime_probs || !theta_out) return fail(HYG_EINVAL, "null argument");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
   if (n_chains <= 0) return HYG_OK;
   if (psi_capacity < 0 || psi_capacity > (1 << 24)) return fail(HYG_EINVAL, "psi_capacity out of range");
   hyg_sgpe_consts pc{};
@@ -616,7 +676,7 @@ int hyg_sg_run_chains_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, cons
     return fail(HYG_EDEVICE, "upload failed");
   }
   uint8_t* ws = (uint8_t*)workspace;
-  if (hipMemcpyAsync(ws, cd.data(), sizeof(SgChainDev) * n_chains, hipMemcpyHostToDevice, s) != hipSuccess) {
+  if (m->stage.upload(ws, cd.data(), sizeof(SgChainDev) * n_chains, s) != hipSuccess) {
     (void)hipFreeAsync(dbuf, s);
     return fail(HYG_EDEVICE, "descriptor upload failed");
   }
@@ -640,6 +700,7 @@ int hyg_sg_run_chain_host_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, 
                              double* regime_probs, double* theta_out) {
   if (!m || !pe || !regime_probs || !theta_out || (S > 0 && (!meth || !tot))) return fail(HYG_EINVAL, "null argument");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
   if (T < 1 || S < 0) return fail(HYG_EINVAL, "no sites");
   if (pe->n_steps_without_update < 1) return fail(HYG_EINVAL, "n_steps_without_update < 1");
   for (int64_t i = 0; i < (int64_t)T * S; ++i)

@@ -305,8 +305,8 @@ def aggregate_main(argv: Sequence[str]) -> int:
         d.to_csv(os.path.join(out_dir, name.format(chrom)), sep="\t", compression="gzip")
         return d
 
-    write("creg", "control_regimes_chrom_{}.csv.gz")
-    write("kreg", "case_regimes_chrom_{}.csv.gz")
+    creg_chrom = write("creg", "control_regimes_chrom_{}.csv.gz")
+    kreg_chrom = write("kreg", "case_regimes_chrom_{}.csv.gz")
     merge_chrom = write("merge", "merge_states_chrom_{}.csv.gz")
     # split_probs_chrom = np.mean(merge_states_chrom == 0, axis=1) (:181): from the device counts
     m = torch.from_numpy(np.ascontiguousarray(merge_chrom.to_numpy(), dtype=np.int16)).to(dev)
@@ -321,4 +321,24 @@ def aggregate_main(argv: Sequence[str]) -> int:
     write("obk", "n_meth_reads_case_chrom_{}.csv.gz")
     write("cdur", "control_durations_chrom_{}.csv.gz")
     write("kdur", "case_durations_chrom_{}.csv.gz")
+    if f["compute_freqs"]:
+        # aggregate_results.py:208-215: per site, value_counts(normalize=True) of
+        # the regimes over all particles; the frame pandas assembles has one
+        # column per regime seen at any site (sorted labels), NaN where a row
+        # has none. The regime histograms come from the device counts kernel.
+        cr = torch.from_numpy(np.ascontiguousarray(creg_chrom.to_numpy(), dtype=np.int16)).to(dev)
+        kr = torch.from_numpy(np.ascontiguousarray(kreg_chrom.to_numpy(), dtype=np.int16)).to(dev)
+        Kf = int(max(int(cr.max().item()), int(kr.max().item()))) + 1
+        if Kf > 16 or int(min(cr.min().item(), kr.min().item())) < 0:
+            raise ValueError("regime labels outside [0, 16)")
+        ctl = torch.stack([torch.zeros_like(cr), cr], dim=2).contiguous()
+        cas = torch.stack([torch.zeros_like(kr), kr], dim=2).contiguous()
+        cnt, _ = site_counts(torch.zeros_like(cr), ctl, cas, Pc, Kf, [(0, Tc)], [[0]], Tc)
+        cnt = cnt.cpu().numpy().astype(np.int64)
+        for g, name in ((1, "case_regimes_freq_{}.csv"), (0, "control_regimes_freq_{}.csv")):
+            h = cnt[:, 2 + g * Kf:2 + (g + 1) * Kf]
+            seen = [r for r in range(Kf) if h[:, r].any()]
+            fr = pd.DataFrame({r: np.where(h[:, r] > 0, h[:, r] / Pc, np.nan) for r in seen},
+                              index=creg_chrom.index)
+            fr.to_csv(os.path.join(out_dir, name.format(chrom)), sep="\t")
     return 0

@@ -139,10 +139,16 @@ def run(observations: Dict[str, np.ndarray], n_total_reads: Dict[str, np.ndarray
 class DeviceChains:
     """Batched device-resident execution of many chains (the bench and the
     multi-chain driver): emission table, history workspace and outputs are
-    torch tensors on the current HIP device; kernels go to `stream`."""
+    torch tensors on the current HIP device; kernels go to `stream`.
+    `workspace` (uint8 tensor) lets batches that run one after another on one
+    stream share the forward->backward history buffer."""
+
+    @staticmethod
+    def workspace_bytes(model: CaseControlModel, chains) -> int:
+        return int(_lib.load().hyg_tg_workspace_bytes(model.handle, len(chains), sum(int(c[1]) for c in chains)))
 
     def __init__(self, model: CaseControlModel, chains: List[Tuple[int, int, int, int, int]], n_out_rows: int,
-                 device=None, final_weights: bool = False):
+                 device=None, final_weights: bool = False, workspace=None):
         import torch
 
         self.torch = torch
@@ -160,7 +166,12 @@ class DeviceChains:
         L = _lib.load()
         self.ws_bytes = int(L.hyg_tg_workspace_bytes(model.handle, len(chains), total))
         dev = self.device
-        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+        if workspace is not None:  # shared with other DeviceChains run one after another on one stream
+            if workspace.numel() < self.ws_bytes or workspace.dtype != torch.uint8:
+                raise ValueError(f"workspace of {workspace.numel()} bytes < {self.ws_bytes} needed")
+            self.ws = workspace
+        else:
+            self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
         self.merged = torch.empty((n_out_rows, B), dtype=torch.int16, device=dev)
         self.control = torch.empty((n_out_rows, B, 2), dtype=torch.int16, device=dev)
         self.case = torch.empty((n_out_rows, B, 2), dtype=torch.int16, device=dev)

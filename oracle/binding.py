@@ -129,6 +129,9 @@ def lib() -> C.CDLL:
         L.oracle_tg_emission.argtypes = [C.POINTER(TgParams), vp, vp, i32, vp, vp, i32, C.c_int64, vp]
         L.oracle_tg_chain.restype = i32
         L.oracle_tg_chain.argtypes = [C.POINTER(TgParams), vp, i32, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.oracle_tg_chain_refstruct.restype = i32
+        L.oracle_tg_chain_refstruct.argtypes = [C.POINTER(TgParams), vp, vp, i32, vp, vp, i32, i32, u64, u64, vp, vp,
+                                                vp, vp, vp, vp]
         L.oracle_tg_trans.restype = d
         L.oracle_tg_trans.argtypes = [C.POINTER(TgParams), i32, u64, u64]
         L.oracle_tg_xi.restype = u64
@@ -197,6 +200,29 @@ def chain(p: TgParams, E: np.ndarray, seed: int, chain_id: int, want_modes: bool
     out["log_z"] = logz.value
     if want_modes:
         out["modes"] = modes
+    return out
+
+
+def chain_refstruct(p: TgParams, meth_c, tot_c, meth_k, tot_k, seed: int, chain_id: int) -> dict:
+    """The reference-structure CPU variant (oracle_tg_chain_refstruct): per-particle
+    Beta-Binomial from the counts, full sort, full-N history, [B, N] backward
+    rows. Same outputs as chain() on the same counts."""
+    mc, tc, mk, tk = (np.ascontiguousarray(a, dtype=np.uint16) for a in (meth_c, tot_c, meth_k, tot_k))
+    T = tc.shape[0]
+    K, B = p.n_regimes, p.num_samples_backward
+    out = {
+        "merged": np.empty((T, B), np.int16),
+        "control": np.empty((T, B, 2), np.int16),
+        "case": np.empty((T, B, 2), np.int16),
+        "split_probs": np.empty(T, np.float32),
+        "regime_probs": np.empty((T, 2 * K), np.float32),
+    }
+    logz = C.c_double(0.0)
+    out["status"] = lib().oracle_tg_chain_refstruct(
+        C.byref(p), _ptr(mc), _ptr(tc), tc.shape[1], _ptr(mk), _ptr(tk), tk.shape[1], T, seed, chain_id,
+        _ptr(out["merged"]), _ptr(out["control"]), _ptr(out["case"]), _ptr(out["split_probs"]),
+        _ptr(out["regime_probs"]), C.byref(logz))
+    out["log_z"] = logz.value
     return out
 
 

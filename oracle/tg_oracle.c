@@ -596,3 +596,126 @@ double oracle_u192_roundtrip(float m) { return hyg_u192_to_f64(hyg_fix149f(m)); 
 double oracle_u128_roundtrip(double e) { return hyg_u128_to_f64(hyg_fix100(e), 100); }
 int oracle_sizeof_params(void) { return (int)sizeof(hyg_tg_params); }
 int oracle_sizeof_consts(void) { return (int)sizeof(hyg_tg_consts); }
+
+/* ------------------------------------------- reference-structure variant */
+/* The same chain (same draws, same outputs bit for bit) computed with the
+ * reference's data structure and work per step, for the CPU baseline of
+ * bench.py:
+ *  - the Beta-Binomial observation density is evaluated per particle from the
+ *    read counts (6 lgamma per sample; case_control_regime_model.py:197-231),
+ *    not looked up in a per-site table;
+ *  - all N candidates are sorted every step (tf.argsort, resampling_functions.py:8);
+ *  - the whole particle system of every step (states + weights, N_max each)
+ *    is kept for the backward pass, as the TensorArrays of
+ *    filter_and_smoother_algorithm.py:291-330 keep it;
+ *  - the backward pass builds one row of N transition log-densities per
+ *    trajectory ([B, N] logits per step, filter_and_smoother_algorithm.py:400-435).
+ * Counts are [T][S] row-major uint16 per group. */
+int oracle_tg_chain_refstruct(const hyg_tg_params* p, const uint16_t* meth_c, const uint16_t* tot_c, int s_c,
+                              const uint16_t* meth_k, const uint16_t* tot_k, int s_k, int T, uint64_t seed,
+                              uint64_t chain_id, int16_t* merged, int16_t* control, int16_t* kase, float* split,
+                              float* regime, double* log_z) {
+  if (T < 1 || T >= HYG_DMAX - 2) return HYG_EINVAL;
+  for (int64_t i = 0; i < (int64_t)T * s_c; ++i) if (meth_c[i] > tot_c[i]) return HYG_EINVAL;
+  for (int64_t i = 0; i < (int64_t)T * s_k; ++i) if (meth_k[i] > tot_k[i]) return HYG_EINVAL;
+  oracle_model om;
+  int rc = om_init(&om, p, T + 2);
+  if (rc) return rc;
+  const hyg_tg_consts* c = &om.c;
+  const int K = c->K, M = c->M, B = c->B, Nmax = c->Nmax;
+  const count_rows counts = {meth_c, tot_c, meth_k, tot_k, s_c, s_k};
+  chain_ctx cx;
+  cx.om = &om;
+  cx.E = NULL;
+  cx.counts = &counts;
+  cx.T = T;
+  cx.rec = (step_rec*)calloc((size_t)T, sizeof(step_rec));
+  cx.par_state = (uint64_t*)calloc((size_t)T * M, sizeof(uint64_t));
+  cx.par_w = (double*)calloc((size_t)T * M, sizeof(double));
+  uint64_t* hst = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)T * Nmax); /* full history */
+  double* hw = (double*)malloc(sizeof(double) * (size_t)T * Nmax);
+  int* hn = (int*)malloc(sizeof(int) * (size_t)T);
+  float* lw32 = (float*)malloc(sizeof(float) * Nmax);
+  uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * Nmax);
+  float* mass = (float*)malloc(sizeof(float) * Nmax);
+  hyg_u192* revcum = (hyg_u192*)malloc(sizeof(hyg_u192) * (Nmax + 1));
+  int* parents = (int*)malloc(sizeof(int) * (M > Nmax ? M : Nmax));
+  double* logits = (double*)malloc(sizeof(double) * Nmax);
+  hyg_u128* cdfa = (hyg_u128*)malloc(sizeof(hyg_u128) * Nmax);
+  uint64_t* X = (uint64_t*)malloc(sizeof(uint64_t) * B);
+  if (!cx.rec || !cx.par_state || !cx.par_w || !hst || !hw || !hn || !lw32 || !keys || !mass || !revcum ||
+      !parents || !logits || !cdfa || !X) {
+    rc = HYG_ENOMEM;
+    goto done;
+  }
+  cx.rec[0].mode = MODE_INIT;
+  cx.rec[0].r_ph = (int)hyg_mulhi64(hyg_rand64(seed, chain_id, HYG_RNG_PHANTOM, 0, 0), (uint64_t)K);
+  hn[0] = gen_particles(&cx, 0, hst, hw);
+  for (int t = 1; t < T; ++t) {
+    const uint64_t* st = hst + (size_t)(t - 1) * Nmax;
+    const double* W = hw + (size_t)(t - 1) * Nmax;
+    rc = resample_step(&cx, t, st, W, hn[t - 1], seed, chain_id, lw32, keys, mass, revcum, parents);
+    if (rc) goto done;
+    hn[t] = gen_particles(&cx, t, hst + (size_t)t * Nmax, hw + (size_t)t * Nmax);
+  }
+  {
+    double mx, logS;
+    lse_exact(hw + (size_t)(T - 1) * Nmax, hn[T - 1], &mx, &logS);
+    if (mx == -INFINITY) { rc = HYG_ENUMERIC; goto done; }
+    *log_z = logS + mx;
+  }
+  for (int t = T - 1; t >= 0; --t) {
+    const uint64_t* st = hst + (size_t)t * Nmax;
+    const double* W = hw + (size_t)t * Nmax;
+    const int N = hn[t];
+    for (int b = 0; b < B; ++b) {
+      const double* row = W;
+      if (t != T - 1) {
+        for (int n = 0; n < N; ++n) {
+          const double f = hyg_isfinite(W[n]) ? tg_trans(&om, st[n], X[b]) : -INFINITY;
+          logits[n] = (hyg_isfinite(f) && hyg_isfinite(W[n])) ? f + W[n] : -INFINITY;
+        }
+        row = logits;
+      }
+      double lmax = -INFINITY;
+      for (int n = 0; n < N; ++n) if (row[n] > lmax) lmax = row[n];
+      if (lmax == -INFINITY) { rc = HYG_ENUMERIC; goto done; }
+      hyg_u128 run = hyg_u128_zero();
+      for (int n = 0; n < N; ++n) { run = hyg_u128_add(run, hyg_fix100(hyg_exp(row[n] - lmax))); cdfa[n] = run; }
+      const uint64_t rnd = hyg_rand64(seed, chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
+      const hyg_u128 target = hyg_scale_target(rnd, run);
+      int lo = 0, hi = N - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (hyg_u128_lt(target, cdfa[mid])) hi = mid; else lo = mid + 1;
+      }
+      parents[b] = lo;
+    }
+    int n_split = 0, nc[HYG_KMAX], nk[HYG_KMAX];
+    for (int r = 0; r < K; ++r) nc[r] = nk[r] = 0;
+    for (int b = 0; b < B; ++b) {
+      const uint64_t x = st[parents[b]];
+      X[b] = x;
+      const size_t o = (size_t)t * B + b;
+      merged[o] = (int16_t)hyg_st_m(x);
+      control[2 * o + 0] = (int16_t)hyg_st_dc(x);
+      control[2 * o + 1] = (int16_t)hyg_st_rc(x);
+      kase[2 * o + 0] = (int16_t)hyg_st_dk(x);
+      kase[2 * o + 1] = (int16_t)hyg_st_rk(x);
+      n_split += (hyg_st_m(x) == 0);
+      nc[hyg_st_rc(x)]++;
+      nk[hyg_st_rk(x)]++;
+    }
+    split[t] = (float)n_split / (float)B;
+    for (int r = 0; r < K; ++r) {
+      regime[(size_t)t * 2 * K + r] = (float)nc[r] / (float)B;
+      regime[(size_t)t * 2 * K + K + r] = (float)nk[r] / (float)B;
+    }
+  }
+  rc = HYG_OK;
+done:
+  free(cx.rec); free(cx.par_state); free(cx.par_w); free(hst); free(hw); free(hn); free(lw32); free(keys);
+  free(mass); free(revcum); free(parents); free(logits); free(cdfa); free(X);
+  om_free(&om);
+  return rc;
+}

@@ -10,6 +10,7 @@ only). Saved as data in tests/golden/dmp_fdr.npz:
     case_<i>_fdr    [k, Q_k, threshold]            (FDR_procedure)
     case_<i>_widx   ranking_indices[:s] (int64)    (weighted_FDR_procedure, w_fp = 1)
     case_<i>_wsum   Nsums[s - 1]
+    tie_*           one more weighted case whose cutoff falls inside a ranking tie group
 
 Usage: python -B tests/golden/make_dmp_golden.py
 """
@@ -64,6 +65,20 @@ def main():
         blob[f"case_{i}_widx"] = np.sort(np.asarray(widx, dtype=np.int64))
         blob[f"case_{i}_wsum"] = np.float64(wsum)
     blob["n_cases"] = np.int64(len(cases()))
+    # a weighted-FDR cutoff inside a ranking tie group: equally spaced sites
+    # (equal false-negative weights) and P = 10 (few distinct statistics); the
+    # reference ranks with np.argsort's default (unstable) sort, so WHICH tied
+    # sites it selects at the boundary is an accident of numpy's introsort
+    rng = np.random.default_rng(5)
+    n, P, thr = 3000, 10, 0.3
+    c = rng.binomial(P, 0.5, size=n).astype(np.int32)
+    pos = (np.arange(n) * 100 + 1000).astype(np.int64)
+    t = 1.0 - c.astype(np.int64) / P
+    wfn = od.false_negative_weights(pos)
+    widx, wsum = mt.weighted_FDR_procedure(t, fdr_threshold=thr, weights_false_negatives=wfn,
+                                           weights_false_positives=np.ones(n))
+    blob.update(tie_counts=c, tie_P=np.int64(P), tie_thr=np.float64(thr), tie_wfn=wfn,
+                tie_widx=np.sort(np.asarray(widx, dtype=np.int64)), tie_wsum=np.float64(wsum))
     np.savez_compressed(os.path.join(HERE, "dmp_fdr.npz"), **blob)
     print("wrote", os.path.join(HERE, "dmp_fdr.npz"), blob["n_cases"], "cases")
 

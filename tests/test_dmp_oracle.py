@@ -57,3 +57,35 @@ def test_site_counts_definitions():
     assert np.array_equal(out[:, 1], P - np.trace(pairs, axis1=1, axis2=2))
     assert np.array_equal(out[:, 2:2 + K], pairs.sum(2))
     assert np.array_equal(out[:, 2 + K:], pairs.sum(1))
+
+
+def tie_boundary_check(idx, ns, z):
+    """A weighted-FDR cutoff inside a ranking tie group (golden tie_* case).
+    The reference selects ranking_indices[:s] of an UNSTABLE np.argsort, so
+    which tied sites it takes at the boundary is numpy's accident; the
+    restatement (and the GPU radix sort) is stable and takes the lowest site
+    indices of the group. Required: the same s and Nsums[s-1], the same sites
+    outside the boundary tie group, and the same number from inside it."""
+    c, P, thr, wfn = z["tie_counts"], int(z["tie_P"]), float(z["tie_thr"]), z["tie_wfn"]
+    t = od.statistics_from_counts(c, P)
+    rk = (t - thr) / (wfn * (1 - t) + np.abs(t - thr))
+    ref = z["tie_widx"]
+    assert len(idx) == len(ref) and ns == z["tie_wsum"]
+    edge = rk[ref].max()
+    group = rk == edge
+    assert group.sum() > 1 and (~group[ref]).sum() < len(ref)  # the cutoff is inside a tie group
+    sel = np.zeros(len(c), bool)
+    sel[idx] = True
+    want = np.zeros(len(c), bool)
+    want[ref] = True
+    np.testing.assert_array_equal(sel[~group], want[~group])
+    assert sel[group].sum() == want[group].sum()
+    return sel, want
+
+
+def test_weighted_fdr_tie_at_cutoff_vs_reference_golden():
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "dmp_fdr.npz"))
+    t = od.statistics_from_counts(z["tie_counts"], int(z["tie_P"]))
+    idx, ns = od.weighted_fdr_procedure(t, float(z["tie_thr"]), np.ones(t.shape[0]), z["tie_wfn"])
+    sel, want = tie_boundary_check(idx, ns, z)
+    assert not np.array_equal(sel, want)  # the accident is real: the sets differ inside the group

@@ -54,3 +54,25 @@ def test_make_bed_file_end_to_end(lib, tmp_path):
                    "--output_file", str(out)])
     assert rc == 0
     assert out.read_bytes() == r_make_bed("21", pos, np.round(probs, 7), cols)
+
+
+@pytest.mark.parametrize("K", [6, 4])
+def test_labels_on_an_8_byte_aligned_view(lib, K):
+    """hyg_bed_labels takes any device pointer: a view at an odd element offset
+    (8- but not 16-byte aligned) must take the scalar-load path."""
+    from hygeia_amd import _lib
+
+    n = 5001
+    probs = regimes_probs(n, K, 99)
+    buf = torch.zeros(n * K + 1, dtype=torch.float64, device="cuda")
+    view = buf[1:].view(n, K)
+    view.copy_(torch.from_numpy(probs).cuda())
+    assert view.data_ptr() % 16 == 8
+    lab = torch.empty(n, dtype=torch.int8, device="cuda")
+    sc = torch.empty(n, dtype=torch.float64, device="cuda")
+    _lib.check(lib.hyg_bed_labels(view.data_ptr(), K, n, lab.data_ptr(), sc.data_ptr(),
+                                  C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    rl, rs = r_labels(probs)
+    np.testing.assert_array_equal(lab.cpu().numpy(), rl)
+    np.testing.assert_array_equal(sc.cpu().numpy(), rs)

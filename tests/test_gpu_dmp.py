@@ -194,7 +194,8 @@ def test_aggregate_cli_end_to_end(tmp_path):
     N = 10 * 48
     out = tmp_path / "agg"
     assert cli.main(["aggregate", "--results_dir", str(tmp_path / "res"), "--chrom", "9", "--seeds", "2",
-                     "--num_particles", str(N), "--output_dir", str(out), "--num_batches", "5"]) == 0
+                     "--num_particles", str(N), "--output_dir", str(out), "--num_batches", "5",
+                     "--compute_freqs"]) == 0
     merged, ctrl = [], []
     for batch in (0, 1):
         d = tmp_path / "res" / f"chrom_9_{batch}"
@@ -209,3 +210,32 @@ def test_aggregate_cli_end_to_end(tmp_path):
     np.testing.assert_array_equal(cr, ctrl[:, :, 1])
     ms = pd.read_csv(out / "merge_states_chrom_9.csv.gz", sep="\t").set_index("pos").to_numpy()
     np.testing.assert_array_equal(ms, merged)
+    # --compute_freqs (aggregate_results.py:208-215): the reference's own pandas
+    # expression on the written regime frames gives the same files
+    for g in ("case", "control"):
+        reg = pd.read_csv(out / f"{g}_regimes_chrom_9.csv.gz", sep="\t").set_index("pos").astype(np.int8)
+        want = reg.apply(lambda x: x.value_counts(normalize=True), 1)
+        assert (out / f"{g}_regimes_freq_9.csv").read_text() == want.to_csv(sep="\t")
+
+
+def test_weighted_fdr_tie_at_cutoff_vs_reference_golden():
+    """The reference's selection at a cutoff inside a tie group depends on
+    np.argsort's unstable order; the device ranking is stable (lowest site
+    indices of the group). Same s, same Nsums[s-1], same sites outside the
+    group, same number from inside it (tests/test_dmp_oracle.py)."""
+    import sys
+
+    from hygeia_amd import dmp
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_dmp_oracle import tie_boundary_check
+
+    z = np.load(GOLD)
+    c, P = z["tie_counts"], int(z["tie_P"])
+    wfn = _dev(z["tie_wfn"], torch.float64)
+    idx, ns = dmp.weighted_fdr(_dev(c.reshape(-1, 1), torch.int32), 0, P, float(z["tie_thr"]),
+                               torch.ones_like(wfn), wfn)
+    tie_boundary_check(np.asarray(idx), ns, z)
+    t = od.statistics_from_counts(c, P)
+    oidx, _ = od.weighted_fdr_procedure(t, float(z["tie_thr"]), np.ones(len(t)), z["tie_wfn"])
+    np.testing.assert_array_equal(idx, oidx)

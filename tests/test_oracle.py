@@ -146,3 +146,16 @@ def test_zero_coverage_is_prior_only(oracle):
     assert out["status"] == 0
     # the prior normalises to 1 up to the float32 model tables (500 steps)
     assert abs(out["log_z"]) < 1e-3
+
+
+@pytest.mark.parametrize("K,M,B,T,S,seed", [(6, 50, 25, 300, 4, 0), (4, 8, 5, 200, 2, 1), (12, 20, 6, 60, 3, 2)])
+def test_reference_structure_variant_equals_oracle(oracle, K, M, B, T, S, seed):
+    """bench.py's reference-structure CPU baseline (per-particle Beta-Binomial,
+    full-N history, [B, N] backward rows) computes the same chain."""
+    d, p, E = _setup(oracle, K, M, B, T, S=S, cov=60.0, dseed=seed + 30)
+    a = oracle.chain(p, E, seed, 5)
+    b = oracle.chain_refstruct(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"], seed, 5)
+    assert a["status"] == 0 and b["status"] == 0
+    for k in OUT_KEYS:
+        assert np.array_equal(a[k], b[k]), k
+    assert a["log_z"] == b["log_z"]

@@ -37,10 +37,11 @@ HBM_PEAK_GBS = 8000.0
 
 
 def bytes_per_site(S: int, K: int) -> int:
-    """Unavoidable HBM bytes per site: uint16 counts (2 x S x 2 B) read by the
-    emission kernel, the f64 emission row written and read back (2 x 8K), the
-    f64 regime probabilities written (8K)."""
-    return 4 * S + 16 * K + 8 * K
+    """SURVEY.md 8(d) algorithmic bytes per site: uint16 counts (2 x S x 2 B),
+    the position (4 B) and the f64 regime probabilities written (8K); the f64
+    emission table between the two kernels is an intermediate and not counted
+    (C2: 16 + 4 + 48 = 68 B)."""
+    return 4 * S + 4 + 8 * K
 
 
 def cpu_baseline(meth, tot, chains, params, seconds, threads, pe=False):
@@ -90,7 +91,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=0)
     ap.add_argument("--psi-capacity", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None, help="default: the host cores usable (bench.host_cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--per-sample", action="store_true", help="one chain per (sample, chromosome), S = 1")
     ap.add_argument("--estimate-parameters", action="store_true", help="online parameter estimation (8f-1)")
@@ -222,9 +223,14 @@ def main():
                      "us_per_step_longest_chain": float(kavg[1] * 1000.0 / max(sizes))},
     }
     if not args.no_cpu_baseline:
+        import bench
+
+        host = bench.host_cpus()
         line["cpu_baseline"] = cpu_baseline(meth.cpu().numpy().view(np.uint16), tot.cpu().numpy().view(np.uint16),
-                                            chains, p, args.cpu_seconds, args.cpu_threads, pe=pe is not None)
+                                            chains, p, args.cpu_seconds,
+                                            args.cpu_threads or host["usable"], pe=pe is not None)
         line["cpu_baseline"]["unit"] = line["unit"]
+        line["cpu_baseline"]["host"] = host
     L.hyg_sg_model_destroy(h)
     print(json.dumps(line), flush=True)
 
