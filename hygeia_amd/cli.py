@@ -176,7 +176,24 @@ def segment_index(n_sites: int, batch: int, segment_size: int, buffer_size: int)
 
 
 def _savetxt(path: str, a: np.ndarray) -> None:
-    np.savetxt(path, a, delimiter=",")  # default fmt '%.18e', gzip by extension, as the reference
+    """np.savetxt(path, a, delimiter=",") (default fmt '%.18e', gzip by
+    extension, as the reference writes these files) for integer-valued arrays:
+    the same text, formatted through a table of the distinct values instead of
+    a Python format call per element."""
+    a = np.asarray(a)
+    if a.ndim not in (1, 2) or a.dtype.kind not in "iu" or a.size == 0:
+        np.savetxt(path, a, delimiter=",")
+        return
+    vals, inv = np.unique(a, return_inverse=True)
+    txt = np.array(["%.18e" % float(v) for v in vals], dtype=object)[inv.reshape(a.shape)]
+    lines = txt if a.ndim == 1 else [",".join(r) for r in txt.tolist()]
+    body = ("\n".join(lines) + "\n").encode("latin-1")
+    if path.endswith(".gz"):
+        with gzip.open(path, "wb", compresslevel=6) as fh:  # zlib's default level (numpy's gzip: 9)
+            fh.write(body)
+    else:
+        with open(path, "wb") as fh:
+            fh.write(body)
 
 
 def infer(argv: Sequence[str]) -> int:
@@ -215,11 +232,7 @@ def infer(argv: Sequence[str]) -> int:
         raise AssertionError("methylated reads exceed total reads")
     ret = slice(r0, r1)
 
-    _savetxt(os.path.join(path, "observations_control.csv.gz"), ob_c.astype(np.int16)[ret])
-    _savetxt(os.path.join(path, "observations_case.csv.gz"), ob_k.astype(np.int16)[ret])
-    _savetxt(os.path.join(path, "n_total_reads_control.csv.gz"), nt_c.astype(np.int16)[ret])
-    _savetxt(os.path.join(path, "n_total_reads_case.csv.gz"), nt_k.astype(np.int16)[ret])
-    _savetxt(os.path.join(path, "positions.csv.gz"), pos[ret])
+    _write_batch_inputs(path, ob_c, ob_k, nt_c, nt_k, pos, ret)
 
     from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
 
@@ -259,7 +272,150 @@ def infer(argv: Sequence[str]) -> int:
     return 0
 
 
-COMMANDS = "preprocess get_chrom_segments infer aggregate get_dmps"
+def _write_batch_inputs(path: str, ob_c, ob_k, nt_c, nt_k, pos, ret) -> None:
+    _savetxt(os.path.join(path, "observations_control.csv.gz"), ob_c.astype(np.int16)[ret])
+    _savetxt(os.path.join(path, "observations_case.csv.gz"), ob_k.astype(np.int16)[ret])
+    _savetxt(os.path.join(path, "n_total_reads_control.csv.gz"), nt_c.astype(np.int16)[ret])
+    _savetxt(os.path.join(path, "n_total_reads_case.csv.gz"), nt_k.astype(np.int16)[ret])
+    _savetxt(os.path.join(path, "positions.csv.gz"), pos[ret])
+
+
+MANY_FLAGS = FLAGS_SPEC + [
+    ("batches", "string", "all", "segments to run: 'all' (get_chrom_segments.py: 1 + n // segment_size) or a "
+                                 "comma list"),
+    ("seeds", "string", "0", "inference seeds, a comma list"),
+]
+
+
+def infer_many(argv: Sequence[str]) -> int:
+    """Multi-task `hygeia infer`: every (batch, seed) task of one chromosome in
+    ONE batched launch (hyg_tg_run_chains, one workgroup per chain), writing
+    the same results_dir/chrom_{chrom}_{batch}/ files as the single-task runs
+    `hygeia infer --batch b --seed s` that modules/two_group/4_infer.nf:42-48
+    fans out (flags{seed}.txt as that run's flags, identical trajectories,
+    probabilities and log Z: the chain id is crc32(chrom) << 32 | batch).
+    The chromosome's CSVs are parsed once instead of once per task."""
+    f = parse_flags(argv, MANY_FLAGS)
+    chrom = str(f["chrom"])
+    seeds = [int(x) for x in str(f["seeds"]).split(",") if x != ""]
+    S, buf = int(f["segment_size"]), int(f["buffer_size"])
+    mu = np.array([float(x) for x in f["mu"]], dtype=np.float32)
+    sigma = np.array([float(x) for x in f["sigma"]], dtype=np.float32)
+    K = mu.shape[0]
+    theta = read_theta(str(f["single_group_dir"]), chrom)
+    if theta.shape[0] != K * K:
+        raise ValueError(f"theta_{chrom}.csv.gz holds {theta.shape[0]} values, expected K^2 = {K * K}")
+    dd = str(f["data_dir"])
+    positions = _read_matrix(os.path.join(dd, f"positions_{chrom}.txt.gz"))
+    tot_c = _read_matrix(os.path.join(dd, f"n_total_reads_control_{chrom}.txt.gz")).astype(np.float32)
+    meth_c = _read_matrix(os.path.join(dd, f"n_methylated_reads_control_{chrom}.txt.gz")).astype(np.float32)
+    tot_k = _read_matrix(os.path.join(dd, f"n_total_reads_case_{chrom}.txt.gz")).astype(np.float32)
+    meth_k = _read_matrix(os.path.join(dd, f"n_methylated_reads_case_{chrom}.txt.gz")).astype(np.float32)
+    n = positions.shape[0]
+    batches = (list(range(0, n // S + 1)) if str(f["batches"]) == "all"
+               else [int(x) for x in str(f["batches"]).split(",") if x != ""])
+    tasks = []  # (batch, lo, hi, r0, r1)
+    for b in batches:
+        seg = segment_index(n, b, S, buf)
+        if seg is None:
+            print(f"Batch index is too large for the chromosome (batch {b})")
+            continue
+        (lo, hi), (r0, r1) = seg
+        if np.sum(tot_k[lo:hi] < meth_k[lo:hi]) != 0 or np.sum(tot_c[lo:hi] < meth_c[lo:hi]) != 0:
+            raise AssertionError("methylated reads exceed total reads")
+        tasks.append((b, lo, hi, r0, r1))
+    if not tasks:
+        return 0
+    from concurrent.futures import ThreadPoolExecutor
+
+    pool = ThreadPoolExecutor(max_workers=max(1, min(16, len(os.sched_getaffinity(0)))))
+    writes = []
+    for (b, lo, hi, r0, r1) in tasks:
+        path = os.path.join(str(f["results_dir"]), "chrom_{}_{}".format(chrom, b))
+        os.makedirs(path, exist_ok=True)
+        for sd in seeds:
+            fs = dict(f, batch=b, seed=sd)
+            with open(os.path.join(path, f"flags{sd}.txt"), "w") as fh:
+                fh.write(serialize_flags(fs))
+        writes.append(pool.submit(_write_batch_inputs, path, meth_c[lo:hi], meth_k[lo:hi], tot_c[lo:hi],
+                                  tot_k[lo:hi], positions[lo:hi].astype(np.int64), slice(r0, r1)))
+
+    try:
+        return _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, meth_k, tot_k, pool,
+                               writes)
+    finally:
+        for w in writes:  # zlib releases the GIL: the files compress in parallel
+            w.result()
+        pool.shutdown()
+
+
+def _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, meth_k, tot_k, pool, writes) -> int:
+    import torch
+
+    from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    lo_all, hi_all = min(t[1] for t in tasks), max(t[2] for t in tasks)
+    to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a[lo_all:hi_all], dtype=np.uint16).view(np.int16)).to(dev)  # noqa: E731
+    d_mc, d_tc, d_mk, d_tk = to_dev(meth_c), to_dev(tot_c), to_dev(meth_k), to_dev(tot_k)
+    max_reads = int(max(tot_c[lo_all:hi_all].max(initial=0), tot_k[lo_all:hi_all].max(initial=0)))
+    chains, out = [], 0
+    for (b, lo, hi, r0, r1) in tasks:
+        for sd in seeds:
+            chains.append((lo - lo_all, hi - lo, sd, chain_id(chrom, b), out))
+            out += hi - lo
+    log_z: Dict[tuple, Dict[int, float]] = {}
+    times: Dict[tuple, Dict[int, float]] = {}
+    for M in f["num_resampled_particles"]:
+        print(M)
+        N = int(M) * (2 * K + K * K)
+        model = two_group.CaseControlModel(
+            mu, sigma, theta, minimum_duration=int(f["minimum_duration"]), omega_case=float(f["omega_case"]),
+            merge_log_prob=float(f["merge_log_prob"]), split_prob=float(f["split_prob"]),
+            num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
+            max_total_reads=max_reads, max_duration=max(c[1] for c in chains) + 1,
+            multinomial=bool(f["multinomial"]))
+        t0 = time.time()
+        dc = two_group.DeviceChains(model, chains, out, device=dev)
+        E = dc.emission(d_mc, d_tc, d_mk, d_tk)
+        dc.run(E)
+        torch.cuda.synchronize(dev)
+        dt = time.time() - t0
+        status = dc.status.cpu().numpy()
+        if (status != 0).any():
+            from . import _lib
+
+            raise _lib.HygError(int(status[status != 0][0]), "chains failed")
+        mg, ct, cs = dc.merged.cpu().numpy(), dc.control.cpu().numpy(), dc.case.cpu().numpy()
+        sp, rp, lz = dc.split_probs.cpu().numpy(), dc.regime_probs.cpu().numpy(), dc.log_z.cpu().numpy()
+        i = 0
+        for (b, lo, hi, r0, r1) in tasks:
+            path = os.path.join(str(f["results_dir"]), "chrom_{}_{}".format(chrom, b))
+            for sd in seeds:
+                o, T = chains[i][4], chains[i][1]
+                rows, ret = slice(o, o + T), slice(o + r0, o + r1)
+                for name, arr in ((f"optimal_backward_particles_merged_state_{N}_{sd}", mg[ret]),
+                                  (f"optimal_backward_particles_control_state_{N}_{sd}", ct[ret]),
+                                  (f"optimal_backward_particles_case_state_{N}_{sd}", cs[ret]),
+                                  (f"optimal_split_probs_{N}_{sd}", sp[rows]),
+                                  (f"optimal_regime_probs_{N}_{sd}", rp[rows])):
+                    writes.append(pool.submit(np.savez_compressed, os.path.join(path, name), arr))
+                log_z.setdefault((b, sd), {})[N] = float(lz[i])
+                times.setdefault((b, sd), {})[N] = dt * T / out  # the launch's wall time, pro rata
+                i += 1
+        model.close()
+    for (b, sd), v in log_z.items():
+        path = os.path.join(str(f["results_dir"]), "chrom_{}_{}".format(chrom, b))
+        with open(os.path.join(path, f"log_normalizing_constants_optimal_{sd}.txt"), "w") as fh:
+            print(v, file=fh)
+        with open(os.path.join(path, f"optimal_time_{sd}.txt"), "w") as fh:
+            print(times[(b, sd)], file=fh)
+        with open(os.path.join(path, f"optimal_time_backward_{sd}.txt"), "w") as fh:
+            print({}, file=fh)
+    return 0
+
+
+COMMANDS = "preprocess get_chrom_segments infer infer_many aggregate get_dmps"
 
 
 def main(argv: Sequence[str] = None) -> int:
@@ -268,9 +424,9 @@ def main(argv: Sequence[str] = None) -> int:
         print("Usage: hygeia [command] [arguments...]")
         return 1
     cmd, rest = argv[0], argv[1:]
-    if cmd == "infer":
+    if cmd in ("infer", "infer_many"):
         try:
-            return infer(rest)
+            return infer(rest) if cmd == "infer" else infer_many(rest)
         except FlagError as e:
             print(f"FATAL Flags parsing error: {e}", file=sys.stderr)
             return 1
@@ -307,6 +463,7 @@ def main(argv: Sequence[str] = None) -> int:
         print("Usage: hygeia [command] [arguments...]\n  preprocess - Preprocess BED methylation files (MI355X)\n"
               "  get_chrom_segments - Get chromosome segments\n"
               "  infer     - Run inference on two groups (MI355X)\n"
+              "  infer_many - Every (batch, seed) task of a chromosome in one launch (MI355X)\n"
               "  aggregate - Aggregate results\n  get_dmps  - Get DMPs (Differentially Methylated Positions)\n"
               "  make_bed_file - Regime BED track of a single-group regimes CSV (MI355X)")
         return 0

@@ -116,3 +116,34 @@ def test_infer_writes_inputs_then_refuses_without_gpu(tmp_path):
     obs = np.loadtxt(out / "observations_control.csv.gz", delimiter=",")
     np.testing.assert_array_equal(obs, data["meth_control"][100:200])  # rows [90, 210), returned [10, 110)
     assert (out / "flags7.txt").read_text().startswith("--mu=")
+
+
+def test_infer_many_writes_inputs_then_refuses_without_gpu(tmp_path):
+    """infer_many parses the chromosome once, writes every task's flags and
+    input files, then needs the HIP library and a device (no CPU path)."""
+    _write_inputs(str(tmp_path), "3", 2500)
+    args = ["infer_many", "--chrom", "3", "--segment_size", "1000", "--buffer_size", "50", "--seeds", "1,2",
+            "--data_dir", str(tmp_path / "data"), "--single_group_dir", str(tmp_path / "sg"),
+            "--results_dir", str(tmp_path / "res")]
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible: covered by tests/test_gpu_two_group.py")
+    with pytest.raises(Exception):
+        cli.main(args)
+    for b in (0, 1, 2):
+        d = tmp_path / "res" / f"chrom_3_{b}"
+        assert (d / "flags1.txt").read_text().splitlines()[-4:-2] == [f"--seed=1", f"--batch={b}"]
+        assert (d / "flags2.txt").exists() and (d / "positions.csv.gz").exists()
+
+
+@pytest.mark.parametrize("shape,dtype", [((300, 4), np.int16), ((257,), np.int64), ((5, 1), np.int16)])
+def test_fast_savetxt_matches_numpy(tmp_path, shape, dtype):
+    """The table formatter writes np.savetxt(delimiter=',')'s exact text."""
+    a = np.random.default_rng(3).integers(-5, 30000, size=shape).astype(dtype)
+    cli._savetxt(str(tmp_path / "a.csv.gz"), a)
+    np.savetxt(str(tmp_path / "b.csv.gz"), a, delimiter=",")
+    assert gzip.open(tmp_path / "a.csv.gz").read() == gzip.open(tmp_path / "b.csv.gz").read()
+    cli._savetxt(str(tmp_path / "c.csv"), a)
+    np.savetxt(str(tmp_path / "d.csv"), a, delimiter=",")
+    assert (tmp_path / "c.csv").read_bytes() == (tmp_path / "d.csv").read_bytes()

@@ -238,3 +238,45 @@ def test_cli_infer_end_to_end(tmp_path, oracle):
         txt = (out / "log_normalizing_constants_optimal_3.txt").read_text()
         assert txt.startswith("{960: ")
         assert float(txt.split(":")[1].strip(" }\n")) == pytest.approx(ref["log_z"], rel=1e-15)
+
+
+def test_infer_many_equals_single_task_runs(tmp_path):
+    """`hygeia infer_many` (every (batch, seed) task of a chromosome in one
+    launch) writes the same per-(chrom, batch) directories as the single-task
+    `hygeia infer` runs modules/two_group/4_infer.nf fans out: identical flags
+    files, trimmed trajectories, untrimmed probabilities, log Z and inputs
+    (gzip headers aside: compared decompressed)."""
+    import gzip
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_cli import _write_inputs
+
+    from hygeia_amd import cli
+
+    _write_inputs(str(tmp_path), "5", 2600)
+    common = ["--chrom", "5", "--segment_size", "1000", "--buffer_size", "60", "--num_resampled_particles", "12",
+              "--num_resampled_particles", "20", "--num_samples_backward", "7", "--data_dir", str(tmp_path / "data"),
+              "--single_group_dir", str(tmp_path / "sg")]
+    for b in (0, 1, 2):  # get_chrom_segments: 1 + 2600 // 1000 segments
+        for sd in (0, 4):
+            assert cli.main(["infer", "--batch", str(b), "--seed", str(sd), "--results_dir", str(tmp_path / "one")]
+                            + common) == 0
+    assert cli.main(["infer_many", "--batches", "all", "--seeds", "0,4", "--results_dir", str(tmp_path / "many")]
+                    + common) == 0
+    one, many = tmp_path / "one", tmp_path / "many"
+    assert sorted(p.name for p in one.iterdir()) == sorted(p.name for p in many.iterdir()) == [
+        "chrom_5_0", "chrom_5_1", "chrom_5_2"]
+    for d in one.iterdir():
+        names = sorted(p.name for p in d.iterdir())
+        assert names == sorted(p.name for p in (many / d.name).iterdir())
+        for nm in names:
+            a, b = d / nm, many / d.name / nm
+            if nm.startswith("optimal_time_"):
+                continue  # wall times
+            if nm.endswith(".npz"):
+                np.testing.assert_array_equal(np.load(a)["arr_0"], np.load(b)["arr_0"])
+            elif nm.endswith(".gz"):
+                assert gzip.open(a).read() == gzip.open(b).read(), nm
+            else:  # the flags files name their own --results_dir
+                assert a.read_text().replace(str(one), "R") == b.read_text().replace(str(many), "R"), nm

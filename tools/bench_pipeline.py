@@ -1,0 +1,100 @@
+"""Pipeline-level throughput of the two-group drop-in, gz-CSV parse and result
+files included.
+
+A synthetic chromosome (default 2.4M CpG, the size of chr1 in the 28M
+workload; 4 + 4 samples) is written in the pipeline's input format
+(preprocess_bed.py:463-470: gzip CSVs of float64 counts + theta_{chrom}.csv.gz),
+then timed end to end:
+
+- `hygeia infer_many --batches all --seeds 0,1`: every (segment, seed) task of
+  the chromosome in one launch, the CSVs parsed once;
+- `hygeia infer` for one task (batch 0, seed 0), the unit that
+  modules/two_group/4_infer.nf fans out; its wall time x the number of tasks is
+  the cost of running the fan-out task by task on one GPU.
+
+Prints one JSON line: sites x seeds / s for both, and the split of the
+batched run (parse, launch, writes).
+usage: python tools/bench_pipeline.py [--sites N] [--seeds 0,1] [--workdir DIR]
+"""
+from __future__ import annotations
+
+import argparse
+import gzip
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def write_inputs(d: str, chrom: str, T: int, S: int = 4, K: int = 6):
+    from hygeia_amd import synthetic as syn
+    from hygeia_amd import two_group
+
+    data = syn.simulate(T, S, S, K=K, seed=20251024, coverage=100.0)
+    os.makedirs(os.path.join(d, "data"), exist_ok=True)
+    os.makedirs(os.path.join(d, "sg"), exist_ok=True)
+
+    def save(path, a):  # np.savetxt(fmt='%s') of float64, as preprocess_bed.py writes them
+        with gzip.open(path, "wt", compresslevel=1) as fh:
+            rows = a.astype(np.float64)
+            if rows.ndim == 1:
+                rows = rows[:, None]
+            fh.write("\n".join(",".join(f"{v:.1f}" for v in r) for r in rows.tolist()) + "\n")
+
+    save(os.path.join(d, "data", f"positions_{chrom}.txt.gz"), syn.positions(T))
+    for g in ("control", "case"):
+        save(os.path.join(d, "data", f"n_total_reads_{g}_{chrom}.txt.gz"), data[f"tot_{g}"])
+        save(os.path.join(d, "data", f"n_methylated_reads_{g}_{chrom}.txt.gz"), data[f"meth_{g}"])
+    theta = two_group.uniform_theta(K, 0.8)
+    with gzip.open(os.path.join(d, "sg", f"theta_{chrom}.csv.gz"), "wt") as fh:
+        fh.write("data\n" + "\n".join(repr(float(x)) for x in theta) + "\n")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sites", type=int, default=2_400_000)
+    ap.add_argument("--seeds", default="0,1")
+    ap.add_argument("--workdir", default=None)
+    a = ap.parse_args()
+    from hygeia_amd import cli
+
+    wd = a.workdir or tempfile.mkdtemp(prefix="hyg_pipe_")
+    chrom = "1"
+    t0 = time.perf_counter()
+    write_inputs(wd, chrom, a.sites)
+    t_write = time.perf_counter() - t0
+    print(f"inputs written in {t_write:.1f} s", flush=True)
+    common = ["--chrom", chrom, "--data_dir", os.path.join(wd, "data"), "--single_group_dir", os.path.join(wd, "sg")]
+    seeds = [int(x) for x in a.seeds.split(",")]
+    n_batches = a.sites // 100000 + 1
+    units = a.sites * len(seeds)  # every site is returned by exactly one segment per seed
+    t0 = time.perf_counter()
+    assert cli.main(["infer_many", "--batches", "all", "--seeds", a.seeds, "--results_dir",
+                     os.path.join(wd, "many")] + common) == 0
+    t_many = time.perf_counter() - t0
+    print(f"infer_many done in {t_many:.1f} s", flush=True)
+    t0 = time.perf_counter()
+    assert cli.main(["infer", "--batch", "0", "--seed", str(seeds[0]), "--results_dir", os.path.join(wd, "one")]
+                    + common) == 0
+    t_one = time.perf_counter() - t0
+    tasks = n_batches * len(seeds)
+    line = {"metric": "pipeline CpG sites x seeds / s (hygeia infer, gz CSV in -> result files out)",
+            "sites": a.sites, "seeds": seeds, "tasks": tasks,
+            "infer_many": {"value": units / t_many, "wall_s": t_many},
+            "infer_task_by_task": {"value": units / (t_one * tasks), "wall_s_one_task": t_one,
+                                   "extrapolated_s": t_one * tasks},
+            "input_write_s": t_write}
+    print(json.dumps(line), flush=True)
+    if a.workdir is None:
+        shutil.rmtree(wd, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
