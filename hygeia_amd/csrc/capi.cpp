@@ -490,9 +490,20 @@ int hyg_sg_emission(const hyg_sg_model* m, const uint16_t* meth, const uint16_t*
   return HYG_OK;
 }
 
-static size_t sg_header_bytes(int32_t n_chains) {
+// workspace header: chain descriptors + status words, then the ring control
+// words of every chain (one contiguous block, zeroed before each launch)
+static size_t sg_desc_bytes(int32_t n_chains) {
   const size_t h = (sizeof(SgChainDev) + sizeof(int32_t)) * (size_t)n_chains;
   return (h + 255) / 256 * 256;
+}
+static size_t sg_header_bytes(int32_t n_chains) {
+  return sg_desc_bytes(n_chains) + (kSgCtlBytes * (size_t)n_chains + 255) / 256 * 256;
+}
+// per-chain offsets of the psi region, the ring and the control words
+static void sg_chain_offsets(SgChainDev& d, int i, int32_t n_chains, size_t region, int K, int cap) {
+  d.psi_offset = (int64_t)region;
+  d.ring_offset = (int64_t)(region + sg_psi_region_bytes(K, cap) + sg_lists_bytes(cap));
+  d.ctl_offset = (int64_t)(sg_desc_bytes(n_chains) + kSgCtlBytes * (size_t)i);
 }
 
 size_t hyg_sg_workspace_bytes(const hyg_sg_model* m, int32_t n_chains, int32_t psi_capacity) {
@@ -522,7 +533,7 @@ int hyg_sg_run_chains(const hyg_sg_model* m, const hyg_sg_chain* chains, int32_t
     if (c.site_begin < 0 || c.out_begin < 0) return fail(HYG_EINVAL, "negative chain offset");
     cd[i].site_begin = c.site_begin;
     cd[i].out_begin = c.out_begin;
-    cd[i].psi_offset = (int64_t)off;
+    sg_chain_offsets(cd[i], i, n_chains, off, m->c.K, cap);
     cd[i].seed = c.seed;
     cd[i].chain_id = c.chain_id;
     cd[i].T = c.n_sites;
@@ -536,7 +547,8 @@ int hyg_sg_run_chains(const hyg_sg_model* m, const hyg_sg_chain* chains, int32_t
   if (m->stage.upload(ws, cd.data(), sizeof(SgChainDev) * n_chains, s) != hipSuccess)
     return fail(HYG_EDEVICE, "descriptor upload failed");
   int32_t* st = status ? status : (int32_t*)(ws + sizeof(SgChainDev) * n_chains);
-  int rc = sg_launch_chains(m->dev(), m->c, (const SgChainDev*)ws, n_chains, E, ws, cap, regime_probs, st, stream);
+  int rc = sg_launch_chains(m->dev(), m->c, (const SgChainDev*)ws, n_chains, E, ws, cap, regime_probs, st,
+                            ws + sg_desc_bytes(n_chains), stream);
   if (rc == HYG_EUNSUPPORTED) return fail(rc, "particle arrays exceed the LDS of a CU (K too large)");
   if (rc != HYG_OK) return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
   return HYG_OK;
@@ -642,7 +654,7 @@ int hyg_sg_run_chains_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, cons
     if (c.site_begin < 0 || c.out_begin < 0) return fail(HYG_EINVAL, "negative chain offset");
     cd[i].site_begin = c.site_begin;
     cd[i].out_begin = c.out_begin;
-    cd[i].psi_offset = (int64_t)off;
+    sg_chain_offsets(cd[i], i, n_chains, off, K, cap);
     cd[i].seed = c.seed;
     cd[i].chain_id = c.chain_id;
     cd[i].T = c.n_sites;
@@ -688,7 +700,8 @@ int hyg_sg_run_chains_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, cons
   pd.lgk_stride = max_rcap;
   pd.theta_out = theta_out;
   int32_t* st = status ? status : (int32_t*)(ws + sizeof(SgChainDev) * n_chains);
-  rc = sg_launch_chains(m->dev(), m->c, (const SgChainDev*)ws, n_chains, E, ws, cap, regime_probs, st, stream, &pd);
+  rc = sg_launch_chains(m->dev(), m->c, (const SgChainDev*)ws, n_chains, E, ws, cap, regime_probs, st,
+                        ws + sg_desc_bytes(n_chains), stream, &pd);
   (void)hipFreeAsync(dbuf, s);
   if (rc == HYG_EUNSUPPORTED) return fail(rc, "particle arrays exceed the LDS of a CU (K too large)");
   if (rc != HYG_OK) return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));

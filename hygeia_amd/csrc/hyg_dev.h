@@ -231,6 +231,20 @@ __device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red)
   return s;
 }
 
+// Block-wide OR of a predicate through LDS (no vmcnt drain, unlike
+// __syncthreads_or, so outstanding global stores are not waited for).
+template <int NT>
+__device__ __forceinline__ bool block_or(bool p, unsigned char* red) {
+  const bool w = wave_ballot(p) != 0;
+  if (NT == 64) return w;
+  lds_barrier();
+  if (lane_id() == 0) ((int*)red)[wave_id()] = w ? 1 : 0;
+  lds_barrier();
+  int any = 0;
+  for (int i = 0; i < NT / 64; ++i) any |= ((int*)red)[i];
+  return any != 0;
+}
+
 // Exclusive block scans. The register forms return this thread's exclusive
 // prefix and the block total; the array form writes out[tid] (exclusive) and
 // out[NT] (total) for searches.

@@ -31,6 +31,8 @@ struct SgChainDev {
   int64_t site_begin;
   int64_t out_begin;
   int64_t psi_offset;  // byte offset of the chain's smoothing slots in the workspace
+  int64_t ring_offset; // byte offset of the chain's step-record ring (SMC workgroup -> smoothing workgroup)
+  int64_t ctl_offset;  // byte offset of the chain's ring control words (zeroed before each launch)
   uint64_t seed;
   uint64_t chain_id;
   int32_t T;
@@ -60,20 +62,36 @@ __host__ __device__ inline size_t sg_pe_region_bytes(int K, int rcap) {
   return (b + 255) / 256 * 256;
 }
 
+// The SMC of a chain runs in one workgroup and its online marginal smoothing
+// in a second one (sg_kernels.hip): per step the SMC workgroup publishes a
+// record {N, N_prev, M, t | ancestor + regime [256] u64 | weights [256] f64 |
+// backward kernels [K][256] f64} into a ring of kSgRing slots in the
+// workspace, the smoothing workgroup consumes it.
+constexpr int kSgRing = 32;
+__host__ __device__ inline size_t sg_rec_bytes(int K) {
+  return (16 + 8 * 2 * (size_t)kSgThreads + 8 * (size_t)K * kSgThreads + 255) / 256 * 256;
+}
+constexpr size_t kSgCtlBytes = 16;  // per chain: head (records published), tail (consumed), abort code, pad
+
 // Per-chain workspace: cap psi slots [K][256] f64, then the pending-time lists
-// slot[2][cap] / time[2][cap] (double-buffered), keep[cap], free[cap] (int32).
+// slot[2][cap] / time[2][cap] (double-buffered), keep[cap], free[cap] (int32),
+// then the step-record ring.
 __host__ __device__ inline size_t sg_psi_region_bytes(int K, int cap) {
   return ((sizeof(double) * (size_t)K * kSgThreads * (size_t)cap) + 255) / 256 * 256;
 }
+__host__ __device__ inline size_t sg_lists_bytes(int cap) {
+  return ((sizeof(int32_t) * 6 * (size_t)cap) + 255) / 256 * 256;
+}
 __host__ __device__ inline size_t sg_chain_ws_bytes(int K, int cap) {
-  return sg_psi_region_bytes(K, cap) + ((sizeof(int32_t) * 6 * (size_t)cap) + 255) / 256 * 256;
+  return sg_psi_region_bytes(K, cap) + sg_lists_bytes(cap) + (size_t)kSgRing * sg_rec_bytes(K);
 }
 
 int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint16_t* meth, const uint16_t* tot,
                        int S, int64_t n_sites, double* E, void* stream);
+// ctl: the chains' ring control words (kSgCtlBytes each, contiguous), zeroed here before the launches
 int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
-                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream,
-                     const SgPeDev* pe = nullptr);
+                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* ctl,
+                     void* stream, const SgPeDev* pe = nullptr);
 size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap, bool pe = false);
 
 }  // namespace hyg

@@ -140,9 +140,42 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap, bool pe) {
     l.pei = o; o = sg_align(o + 4 * (2 * HYG_KMAX + 8));
     l.rpu = o; o = sg_align(o + 2 * NT);
   }
+  (void)cap;
+  l.nl = 0;  // the psi slots live in the smoothing workgroup (SgCLay)
+  l.psil = o;
+  l.total = o;
+  return l;
+}
+
+// LDS of the smoothing workgroup: the step record (ancestors, regimes, weights,
+// backward kernels), per-wave scratch, the finalisation buffers, and as many
+// psi slots [K][256] f64 as fit (up to 32; the rest live in the workspace).
+struct SgCLay {
+  size_t anc, rgn, w, BK, scr, meanb, okb, red, sh, psil, total;
+  int nl;
+};
+struct SgCShared {
+  int npend, nfree, cur, status;
+  int avail, abort_code, pad0, pad1;
+  unsigned int lmask;
+  int pad2;
+};
+constexpr size_t kSgLdsBudget = 160 * 1024 - 2048;  // headroom below the 160 KiB of a CU (launches at 163808 B fail)
+__host__ __device__ inline SgCLay sg_clayout(int K, int cap) {
+  SgCLay l{};
+  const int NT = kSgThreads, NB = sg_block_threads(K), NW = NB / 64;
+  size_t o = 0;
+  l.anc = o; o = sg_align(o + 4 * NT);
+  l.rgn = o; o = sg_align(o + NT);
+  l.w = o; o = sg_align(o + 8 * NT);
+  l.BK = o; o = sg_align(o + 8 * (size_t)K * NT);
+  l.scr = o; o = sg_align(o + 8 * (size_t)NW * NT);
+  l.meanb = o; o = sg_align(o + 8 * (size_t)kSgChunk * K);
+  l.okb = o; o = sg_align(o + (size_t)kSgChunk * K);
+  l.red = o; o = sg_align(o + 24 * (size_t)NW * K + 16 * NW + 64);
+  l.sh = o; o = sg_align(o + sizeof(SgCShared));
   const size_t slot = 8 * (size_t)K * NT;
-  const size_t budget = 160 * 1024 - 2048;  // headroom below the 160 KiB of a CU (launches at 163808 B fail)
-  int nl = o < budget ? (int)((budget - o) / slot) : 0;
+  int nl = o < kSgLdsBudget ? (int)((kSgLdsBudget - o) / slot) : 0;
   if (nl > 32) nl = 32;
   if (nl > cap) nl = cap;
   l.nl = nl;
@@ -151,7 +184,35 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap, bool pe) {
   return l;
 }
 
-size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap, bool pe) { return sg_layout(c.K, psi_cap, pe).total; }
+// one launch's dynamic LDS: the larger of the two workgroup roles
+size_t sg_lds_bytes(const hyg_sg_consts& c, int psi_cap, bool pe) {
+  const size_t a = sg_layout(c.K, psi_cap, pe).total, b = sg_clayout(c.K, psi_cap).total;
+  return a > b ? a : b;
+}
+
+// ------------------------------------------------ inter-workgroup hand-off
+// Ring of step records from the SMC workgroup to the smoothing workgroup
+// (cdna_hip_programming.md Guideline 16, recipe R1): every payload word is
+// stored write-through (agent-scope relaxed atomic store = global_store sc1),
+// each storing wave drains its stores (s_waitcnt vmcnt(0)) before a workgroup
+// barrier, then ONE lane stores the head counter; the consumer polls head
+// relaxed, ONE agent-scope acquire, then plain loads. Control words
+// (ctl[0] head = records published, ctl[1] tail = records consumed, ctl[2]
+// abort code) are zeroed by the launch function.
+typedef __attribute__((address_space(1))) unsigned int sg_gu32;
+typedef __attribute__((address_space(1))) unsigned long long sg_gu64;
+constexpr unsigned kSgTailAbort = 0x7fffffffu;  // the smoothing workgroup gave up: never wait for ring space
+constexpr unsigned kSgSpinMax = 1u << 24;       // bounded spins (~25 s of polling): then HYG_EDEVICE
+__device__ __forceinline__ void sg_st8(uint8_t* p, uint64_t v) {
+  __hip_atomic_store((sg_gu64*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sg_st4(uint8_t* p, unsigned v) {
+  __hip_atomic_store((sg_gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned sg_ld4(uint8_t* p) {
+  return __hip_atomic_load((sg_gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sg_drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ------------------------------------------------------------- emission
 // E[t][r] = sum_s log BB(y_ts | n_ts, alpha_r, beta_r) in the oracle's term
@@ -346,17 +407,31 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
 // and backward kernels, and the smoothing split into (pending time, regime)
 // tasks over all waves with the psi rows resident in LDS (up to 32 slots,
 // the rest in the chain's workspace region).
+template <int KT, int NB>
+__device__ __forceinline__ void sg_smoother(const SgModelDev md, const SgChainDev ch, int chain,
+                                            uint8_t* __restrict__ ws, int cap, double* __restrict__ probs,
+                                            int32_t* __restrict__ status_out, const SgCLay lay);
+
 template <int KT, int NB, bool PE>
 __global__ void __launch_bounds__(NB)
-sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const double* __restrict__ E,
+sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chains, const double* __restrict__ E,
                 uint8_t* __restrict__ ws, int cap, double* __restrict__ probs, int32_t* __restrict__ status_out,
-                SgLay lay, unsigned long long* __restrict__ dbg, SgPeDev pe) {
+                SgLay lay, SgCLay clay, unsigned long long* __restrict__ dbg, SgPeDev pe) {
+  // blocks [0, n_chains): the SMC of chain b; blocks [n_chains, 2 n_chains):
+  // the online marginal smoothing of chain b - n_chains, fed by the ring
+  if ((int)blockIdx.x >= n_chains) {
+    const int chain = (int)blockIdx.x - n_chains;
+    sg_smoother<KT, NB>(md, chains[chain], chain, ws, cap, probs, status_out, clay);
+    return;
+  }
   constexpr int NT = kSgThreads, NW = NB / 64, K = KT;  // NT: particle slots, NB: threads
   const hyg_sg_consts& c = *md.consts;
   const int Nmax = c.Nmax, u = c.u, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const double eps = c.epsilon;
   const SgChainDev ch = chains[blockIdx.x];
   const int T = ch.T;
+  uint8_t* ring = ws + ch.ring_offset;
+  uint8_t* ctl = ws + ch.ctl_offset;
+  const size_t rec_bytes = sg_rec_bytes(K);
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t* st_ = (uint32_t*)(smem + lay.st);
   double* lw_ = (double*)(smem + lay.lw);
@@ -375,26 +450,11 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   double* logP = PE ? pm->logP : (double*)(smem + lay.logP);
   unsigned char* red = smem + lay.red;
   double* lsev = (double*)(smem + lay.lsev);
-  double* scr = (double*)(smem + lay.scr) + wv * NT;
-  double* meanb = (double*)(smem + lay.meanb);
-  uint8_t* okb = smem + lay.okb;
-  double* psil = (double*)(smem + lay.psil);
   double* logm = (double*)(smem + lay.logm);
   double* logQ = (double*)(smem + lay.logQ);
   SgShared& sh = *(SgShared*)(smem + lay.sh);
-  const int nl = lay.nl;
-  uint8_t* wbase = ws + ch.psi_offset;
-  double* psig = (double*)wbase;
-  int32_t* lists = (int32_t*)(wbase + sg_psi_region_bytes(K, cap));
-  int32_t* keepf = lists + 4 * (size_t)cap;
-  int32_t* freel = lists + 5 * (size_t)cap;
-  double* out = probs + (size_t)ch.out_begin * K;
   const double* Ech = E + (size_t)ch.site_begin * K;
-  auto slot_row = [&](int slot, int r) -> double* {
-    return slot < nl ? psil + ((size_t)slot * K + r) * NT : psig + ((size_t)(slot - nl) * K + r) * NT;
-  };
 
-  for (int i = tid; i < cap; i += NB) freel[i] = cap - 1 - i;
   if (!PE)
     for (int i = tid; i < K * K; i += NB) logP[i] = c.logP[i];
   // parameter estimation state (OnlineParameterEstimation.h:42-176)
@@ -434,13 +494,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   }
 #define SG_CNT(k, v) \
   if (dbg && tid == 0) sh.ph[k] += (v);
-  if (tid == 0) {
-    sh.npend = 0;
-    sh.nfree = cap;
-    sh.cur = 0;
-    sh.status = HYG_OK;
-    sh.lmask = nl >= 32 ? 0xffffffffu : ((1u << nl) - 1u);
-  }
+  if (tid == 0) sh.status = HYG_OK;
   // ---- t = 0 (Smc.h:114-188): N = K particles (1, r), log w = -log K + log g_0(r)
   int N = K;
   uint32_t my_st = sg_pack(1, tid < K ? tid : 0);
@@ -478,9 +532,13 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
   __syncthreads();
 
   int status = HYG_OK;
+  int tail_seen = 0;  // records the smoothing workgroup has consumed, as last read
+  constexpr int KHr = (NB == 2 * NT) ? (K + 1) / 2 : K;  // backward-kernel rows per thread (see the weights)
+  double BKr[KHr];
+#pragma unroll
+  for (int j = 0; j < KHr; ++j) BKr[j] = 0.0;
   if (dbg && tid == 0) sh.ph[15] = __builtin_amdgcn_s_memtime();
   for (int t = 0; t < T; ++t) {
-    const bool final = (t == T - 1);
     const int cb = t & 1, pb = cb ^ 1;  // LDS buffers of the current / previous particle sets
     int M = 0, Np = N;
     if (t > 0) {
@@ -515,7 +573,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           double q = (tid < Np) ? wP[lidx] : 0.0;
           if (tid < NT) logq[tid] = q;
           lds_barrier();
-          const bool mono = !__syncthreads_or(tid + 1 < Np && logq[tid + 1] > q);
+          const bool mono = !block_or<NB>(tid + 1 < Np && logq[tid + 1] > q, red);
           int idx = lidx;
           if (!mono) {
             uint64_t key = (tid < Np) ? sg_okey(pw) : 0;
@@ -548,8 +606,42 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
           }
           lds_barrier();
           SG_PH(1);
-          // the K / log c fixed point (:333-342) in wave 0: counts by ballot
-          if (wv == 0) {
+          // the K / log c fixed point (:333-342). When log q is non-increasing
+          // along the sorted order (checked; log is only nearly monotone), the
+          // count #{p >= a : log q_p > -c(a)} is a prefix length: every a in
+          // [0, Np] gets c(a) and its successor next(a) by a binary search at
+          // once, then one lane follows a -> next(a) from 0 to the fixed point
+          // (the loop's iterates, so K and log c are the loop's). Otherwise the
+          // loop runs in wave 0 with counts by ballot.
+          const bool lqmono = !block_or<NB>(tid + 1 < Np && logq[tid + 1] > logq[tid], red);
+          if (lqmono) {
+            double* cval = (double*)cum;           // [NT + 1] c(a)
+            int* nxt = (int*)(cval + NT + 1);      // [NT + 1] next(a)
+            for (int a = tid; a <= Np; a += NB) {
+              const int mk = M - a;
+              const double cA = (mk >= 0 ? logm[mk] : HYG_NAN) - logQ[a];
+              const double thr = -cA;
+              int lo = 0, hi = Np;  // first p with !(log q_p > thr)
+              while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (logq[mid] > thr) lo = mid + 1; else hi = mid;
+              }
+              nxt[a] = a + (lo > a ? lo - a : 0);
+              cval[a] = cA;
+            }
+            lds_barrier();
+            if (tid == 0) {
+              int kOld = 1, kNew = 0, iters = 0;
+              while (kNew != kOld) {
+                kOld = kNew;
+                kNew = nxt[kOld];
+                ++iters;
+              }
+              sh.Kk = kNew;
+              sh.logC = cval[kOld];
+              SG_CNT(10, iters);
+            }
+          } else if (wv == 0) {
             double lq4[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) lq4[i] = logq[lane + 64 * i];
@@ -651,65 +743,80 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       // x_qn = W_prev[n] + log f((1,q) | n), and the fresh particles (1, q) with
       // log weight max_q + log S_q + log g_t(q): thread n = previous particle n,
       // the K row reductions batched (oracle/sg_oracle.c)
-      double vb[K];
+      // With 512 threads (K <= 8) thread n < 256 takes rows [0, KH) of previous
+      // particle n and thread 256 + n rows [KH, K) (its particle read from LDS):
+      // half of the rows per thread, same values, exact sums.
+      constexpr bool SPLIT = (NB == 2 * NT);
+      constexpr int KH = SPLIT ? (K + 1) / 2 : K;
+      const int pn = SPLIT ? (tid & (NT - 1)) : tid;  // the previous particle of this thread
+      const int q0 = (SPLIT && tid >= NT) ? KH : 0;   // wave-uniform
+      double vb[KH];
       {
-        const bool live = tid < Np;
-        const int rp = sg_r(pst);
+        double vlw = plw, vbase = pbase;
+        uint32_t vst = pst;
+        if (SPLIT && tid >= NT) {
+          vlw = lwP[pn];
+          vbase = base_[pb * NT + pn];
+          vst = stP[pn];
+        }
+        const bool live = pn < Np;
+        const int rp = sg_r(vst);
 #pragma unroll
-        for (int q = 0; q < K; ++q) vb[q] = live ? plw + (pbase + logP[rp * K + q]) : HYG_NINF;
+        for (int j = 0; j < KH; ++j) {
+          const int q = q0 + j;
+          vb[j] = (live && q < K) ? vlw + (vbase + logP[rp * K + q]) : HYG_NINF;
+        }
       }
       double* redd = (double*)red;
       hyg_u128* redu = (hyg_u128*)(red + 8 * NW * K);
-      // waves >= 4 of a 512-thread group hold no particle: they write neutral
-      // partials (-inf maxima, zero sums) instead of reducing -inf rows
-      const bool realw = (NB == NT) || wv < NT / 64;
-      double mq[K];
+      double mq[KH];
 #pragma unroll
-      for (int q = 0; q < K; ++q) mq[q] = HYG_NINF;
-      if (realw) {
+      for (int j = 0; j < KH; ++j) mq[j] = wave_max(vb[j]);
+      if (lane == 0) {  // rows this wave does not take: neutral partials (-inf maxima, zero sums)
 #pragma unroll
-        for (int q = 0; q < K; ++q) mq[q] = wave_max(vb[q]);
-      }
-      if (lane == 0) {
+        for (int q = 0; q < K; ++q) {
+          double v = HYG_NINF;
 #pragma unroll
-        for (int q = 0; q < K; ++q) redd[wv * K + q] = mq[q];
+          for (int j = 0; j < KH; ++j) v = (q0 + j == q) ? mq[j] : v;
+          redd[wv * K + q] = v;
+        }
       }
       lds_barrier();
 #pragma unroll
-      for (int q = 0; q < K; ++q) {
+      for (int j = 0; j < KH; ++j) {
+        const int q = q0 + j < K ? q0 + j : K - 1;
         double m = redd[q];
 #pragma unroll
         for (int w = 1; w < NW; ++w) m = dmax(m, redd[w * K + q]);
-        mq[q] = m;
+        mq[j] = (q0 + j < K) ? m : HYG_NINF;
       }
-      double ev[K];
+      double ev[KH];
       {
-        hyg_u128 s2[K];
+        hyg_u128 s2[KH];
 #pragma unroll
-        for (int q = 0; q < K; ++q) {
-          ev[q] = 0.0;
-          s2[q] = hyg_u128_zero();
+        for (int j = 0; j < KH; ++j) {
+          ev[j] = hyg_exp(vb[j] - mq[j]);
+          s2[j] = hyg_fix100(ev[j]);
         }
-        if (realw) {
 #pragma unroll
-          for (int q = 0; q < K; ++q) {
-            ev[q] = hyg_exp(vb[q] - mq[q]);
-            s2[q] = hyg_fix100(ev[q]);
-          }
-#pragma unroll
-          for (int q = 0; q < K; ++q) s2[q] = wave_sum128(s2[q]);
-        }
+        for (int j = 0; j < KH; ++j) s2[j] = wave_sum128(s2[j]);
         if (lane == 0) {
 #pragma unroll
-          for (int q = 0; q < K; ++q) redu[wv * K + q] = s2[q];
+          for (int q = 0; q < K; ++q) {
+            hyg_u128 v = hyg_u128_zero();
+#pragma unroll
+            for (int j = 0; j < KH; ++j) {
+              v.lo = (q0 + j == q) ? s2[j].lo : v.lo;
+              v.hi = (q0 + j == q) ? s2[j].hi : v.hi;
+            }
+            redu[wv * K + q] = v;
+          }
         }
       }
       lds_barrier();
       if (tid < K) {
-        double m = HYG_NINF;
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-          if (q == tid) m = mq[q];
+        double m = redd[tid];
+        for (int w = 1; w < NW; ++w) m = dmax(m, redd[w * K + tid]);
         hyg_u128 s = hyg_u128_zero();
         for (int w = 0; w < NW; ++w) s = hyg_u128_add(s, redu[w * K + tid]);
         const double S = hyg_u128_to_f64(s, 100);
@@ -717,9 +824,11 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         lsev[K + tid] = (m > HYG_NINF) ? 1.0 / S : 0.0;
       }
       lds_barrier();
-      if (tid < Np) {
 #pragma unroll
-        for (int q = 0; q < K; ++q) BK[q * NT + tid] = (lsev[q] > HYG_NINF) ? ev[q] * lsev[K + q] : 0.0;
+      for (int j = 0; j < KH; ++j) {  // this thread's entries of the backward kernels (record of step t)
+        const int q = q0 + j < K ? q0 + j : K - 1;
+        BKr[j] = (q0 + j < K && lsev[q] > HYG_NINF) ? ev[j] * lsev[K + q] : 0.0;
+        if (PE && pn < Np && q0 + j < K) BK[q * NT + pn] = BKr[j];
       }
       if (tid >= M && tid < N) {
         const int q = tid - M;
@@ -732,6 +841,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       }
       SG_PH(4);
       // ---- selfNormaliseWeights (:576-579)
+      // record t-1 (stored at the end of step t-1) is drained by every wave
+      // here, before the barriers of the reductions; published after them
+      sg_drain_stores();
       double mx;
       block_max_cnt<NB>(nlw, (tid < N && hyg_isfinite(nlw)) ? 1 : 0, red, &mx, &fin);
       if (!(mx > HYG_NINF)) {
@@ -740,9 +852,10 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       }
       {
         hyg_u128 fx = hyg_u128_zero();
-        if (realw) fx = hyg_fix100(hyg_exp(nlw - mx));
+        if ((NB == NT) || wv < NT / 64) fx = hyg_fix100(hyg_exp(nlw - mx));  // waves >= 4 hold no particle
         logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NB>(fx, red), 100));
       }
+      if (tid == 0) sg_st4(ctl, (unsigned)t);  // records 0 .. t-1 are published
       my_lw = nlw;
       my_st = nst;
       my_w = 0.0;
@@ -912,6 +1025,165 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         SG_PH(12);
       }
     }
+    // ---- hand the step to the smoothing workgroup (OnlineMarginalSmoothing::update
+    //      consumes exactly these: ancestors, regimes, self-normalised weights and
+    //      the backward kernels of step t): record t into ring slot t % kSgRing,
+    //      once the smoothing workgroup has consumed record t - kSgRing
+    if (t - kSgRing + 1 > tail_seen) {  // re-read the tail only when the cached value is not enough
+      unsigned spins = 0, tl;
+      while ((tl = sg_ld4(ctl + 4)) < (unsigned)(t - kSgRing + 1)) {
+        if (++spins > kSgSpinMax) { tl = kSgTailAbort; break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (tl == kSgTailAbort) {  // the smoothing workgroup stopped (and reports the status)
+        status = HYG_EDEVICE;
+        break;
+      }
+      tail_seen = (int)tl;
+    }
+    {
+      uint8_t* rec = ring + (size_t)(t % kSgRing) * rec_bytes;
+      if (tid == 0) {
+        sg_st8(rec, (uint64_t)(uint32_t)N | ((uint64_t)(uint32_t)Np << 32));
+        sg_st8(rec + 8, (uint64_t)(uint32_t)M | ((uint64_t)(uint32_t)t << 32));
+      }
+      if (tid < NT) {
+        const int a = (tid < M) ? anc[tid] : 0;
+        const int rg = (tid < N) ? sg_r(my_st) : 0;
+        sg_st8(rec + 16 + 8 * (size_t)tid, (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)rg << 32));
+        sg_st8(rec + 16 + 8 * (size_t)(NT + tid), u_of(tid < N ? my_w : 0.0));
+      }
+      {
+        const int pn = (NB == 2 * NT) ? (tid & (NT - 1)) : tid;
+        const int q0 = (NB == 2 * NT && tid >= NT) ? KHr : 0;
+        if (pn < Np) {
+#pragma unroll
+          for (int j = 0; j < KHr; ++j)
+            if (q0 + j < K) sg_st8(rec + 16 + 8 * (size_t)(2 * NT + (q0 + j) * NT + pn), u_of(BKr[j]));
+        }
+      }
+    }
+    if (tid < N) {
+      base_[cb * NT + tid] = my_base;
+      cont_[cb * NT + tid] = my_cont;
+    }
+    lds_barrier();
+    SG_PH(6);
+  }
+  // publish the last records, or the abort code for the smoothing workgroup
+  sg_drain_stores();
+  __syncthreads();
+  if (tid == 0) {
+    if (status == HYG_OK) sg_st4(ctl, (unsigned)T);
+    else sg_st4(ctl + 8, (unsigned)(-status));
+  }
+
+  if (dbg && tid < 15) dbg[(size_t)blockIdx.x * 16 + tid] = sh.ph[tid];
+  if (dbg && tid == 15) dbg[(size_t)blockIdx.x * 16 + 15] = (unsigned long long)T;
+#undef SG_PH
+#undef SG_CNT
+}
+
+
+// The online marginal smoothing of one chain (OnlineMarginalSmoothing.h:52-255),
+// in its own workgroup: per step t it takes record t of the SMC workgroup
+// (N, N_prev, M, ancestors, regimes, self-normalised weights, backward kernels)
+// from the ring and runs updatePsi of the pending times, initialisePsi of t and
+// storeEstimates with the epsilon rule, as (pending time, regime) tasks over
+// all waves; psi rows live in LDS slots (up to 32) and the chain's workspace.
+// The same operations in the same order as the in-workgroup smoothing of
+// oracle/sg_oracle.c, so the outputs stay bit-identical. Writes status_out.
+template <int KT, int NB>
+__device__ __forceinline__ void sg_smoother(const SgModelDev md, const SgChainDev ch, int chain,
+                                            uint8_t* __restrict__ ws, int cap, double* __restrict__ probs,
+                                            int32_t* __restrict__ status_out, const SgCLay lay) {
+  constexpr int NT = kSgThreads, NW = NB / 64, K = KT;
+  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const double eps = md.consts->epsilon;
+  const int T = ch.T;
+  extern __shared__ __align__(16) unsigned char smem[];
+  int* anc = (int*)(smem + lay.anc);
+  uint8_t* rgn = smem + lay.rgn;
+  double* wC = (double*)(smem + lay.w);
+  double* BK = (double*)(smem + lay.BK);
+  double* scr = (double*)(smem + lay.scr) + wv * NT;
+  double* meanb = (double*)(smem + lay.meanb);
+  uint8_t* okb = smem + lay.okb;
+  unsigned char* red = smem + lay.red;
+  SgCShared& sh = *(SgCShared*)(smem + lay.sh);
+  double* psil = (double*)(smem + lay.psil);
+  const int nl = lay.nl;
+  uint8_t* wbase = ws + ch.psi_offset;
+  double* psig = (double*)wbase;
+  int32_t* lists = (int32_t*)(wbase + sg_psi_region_bytes(K, cap));
+  int32_t* keepf = lists + 4 * (size_t)cap;
+  int32_t* freel = lists + 5 * (size_t)cap;
+  uint8_t* ring = ws + ch.ring_offset;
+  uint8_t* ctl = ws + ch.ctl_offset;
+  const size_t rec_bytes = sg_rec_bytes(K);
+  double* out = probs + (size_t)ch.out_begin * K;
+  auto slot_row = [&](int slot, int r) -> double* {
+    return slot < nl ? psil + ((size_t)slot * K + r) * NT : psig + ((size_t)(slot - nl) * K + r) * NT;
+  };
+  (void)red;
+  for (int i = tid; i < cap; i += NB) freel[i] = cap - 1 - i;
+  if (tid == 0) {
+    sh.npend = 0;
+    sh.nfree = cap;
+    sh.cur = 0;
+    sh.status = HYG_OK;
+    sh.avail = 0;
+    sh.abort_code = 0;
+    sh.lmask = nl >= 32 ? 0xffffffffu : ((1u << nl) - 1u);
+  }
+  __syncthreads();
+  int status = HYG_OK;
+  int avail = 0;
+  for (int t = 0; t < T; ++t) {
+    const bool final = (t == T - 1);
+    if (t >= avail) {
+      // wait for record t: wave 0 polls head (relaxed), ONE agent-scope acquire
+      if (wv == 0) {
+        unsigned h = 0, ab = 0, spins = 0;
+        for (;;) {
+          h = sg_ld4(ctl);
+          ab = sg_ld4(ctl + 8);
+          if ((int)h > t || ab != 0) break;
+          if (++spins > kSgSpinMax) { ab = (unsigned)(-HYG_EDEVICE); break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        sg_drain_stores();
+        if (lane == 0) {
+          sh.avail = (int)h;
+          sh.abort_code = (int)ab;
+        }
+      }
+      __syncthreads();
+      avail = sh.avail;
+      if (avail <= t) {  // the SMC workgroup stopped (its code) or the wait timed out
+        status = sh.abort_code ? -sh.abort_code : HYG_EDEVICE;
+        break;
+      }
+    }
+    // ---- record t into LDS (plain loads behind the acquire)
+    const uint8_t* rec = ring + (size_t)(t % kSgRing) * rec_bytes;
+    // header through vector loads (a wave-uniform plain load could take the scalar cache)
+    const uint64_t h0 = __hip_atomic_load((sg_gu64*)rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t h1 = __hip_atomic_load((sg_gu64*)(rec + 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int N = (int)(uint32_t)h0, Np = (int)(h0 >> 32), M = (int)(uint32_t)h1;
+    for (int i = tid; i < NT; i += NB) {
+      const uint64_t ar = ((const uint64_t*)(rec + 16))[i];
+      anc[i] = (int)(uint32_t)ar;
+      rgn[i] = (uint8_t)(ar >> 32);
+      wC[i] = ((const double*)(rec + 16))[NT + i];
+    }
+    for (int i = tid; i < K * NT; i += NB) {
+      const int n = i - (i / NT) * NT;
+      BK[i] = (n < Np) ? ((const double*)(rec + 16))[2 * NT + i] : 0.0;
+    }
+    __syncthreads();
+    if (tid == 0) sg_st4(ctl + 4, (unsigned)(t + 1));  // slot t % kSgRing may be rewritten
     // ---- online marginal smoothing: updatePsi (OnlineMarginalSmoothing.h:152-197)
     //      of the pending times, initialisePsi (:132-150) of time t, storeEstimates
     //      (:199-253) with the epsilon rule, as (pending time, regime) tasks
@@ -941,10 +1213,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       status = sh.status;
       break;
     }
-    const uint32_t* stC = st_ + cb * NT;
-    const double* wC = w_ + cb * NT;
     const int ntot = nold + 1;
-    SG_CNT(11, ntot);
     for (int c0 = 0; c0 < ntot; c0 += kSgChunk) {
       const int ne = (ntot - c0 < kSgChunk) ? ntot - c0 : kSgChunk;
       for (int task = wv; task < ne * K; task += NW) {
@@ -956,7 +1225,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int n = lane + 64 * i;
-            nv[i] = (n < N && sg_r(stC[n]) == r) ? 1.0 : 0.0;
+            nv[i] = (n < N && (int)rgn[n] == r) ? 1.0 : 0.0;
           }
         } else {
           double pv[4];
@@ -1042,7 +1311,6 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
       }
       __syncthreads();
     }
-    SG_PH(6);
     // compaction of the pending list into the other buffer; freed slots go
     // back to the LDS mask or the workspace free list (order is immaterial)
     {
@@ -1077,32 +1345,37 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, const doub
         sh.nfree = nf;
         sh.cur = cur ^ 1;
       }
-      if (tid < N) {
-        base_[cb * NT + tid] = my_base;
-        cont_[cb * NT + tid] = my_cont;
-      }
       __syncthreads();
-      SG_PH(7);
     }
   }
-  if (tid == 0) status_out[blockIdx.x] = status;
-  if (dbg && tid < 15) dbg[(size_t)blockIdx.x * 16 + tid] = sh.ph[tid];
-  if (dbg && tid == 15) dbg[(size_t)blockIdx.x * 16 + 15] = (unsigned long long)T;
-#undef SG_PH
-#undef SG_CNT
+  if (tid == 0) {
+    if (status != HYG_OK) sg_st4(ctl + 4, kSgTailAbort);  // the SMC workgroup must not wait for ring space
+    status_out[chain] = status;
+  }
 }
 
 // ------------------------------------------------------------- launches
+// One launch per group of at most (CUs / 2) chains: the SMC and the smoothing
+// workgroup of every chain must be co-resident (one workgroup per CU at this
+// LDS size), since each waits for the other through the ring.
 template <int KT, int NB, bool PE>
 static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, int n_chains, const double* E,
                             uint8_t* ws, int cap, double* probs, int32_t* status, const SgLay& lay,
-                            unsigned long long* dbg, hipStream_t s, const SgPeDev& pe, hipError_t* err) {
+                            const SgCLay& clay, size_t lds, unsigned long long* dbg, hipStream_t s, const SgPeDev& pe,
+                            hipError_t* err) {
   *err = hipFuncSetAttribute((const void*)sg_chain_kernel<KT, NB, PE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lay.total);
+                             (int)lds);
   if (*err != hipSuccess) return;
-  hipLaunchKernelGGL((sg_chain_kernel<KT, NB, PE>), dim3(n_chains), dim3(NB), lay.total, s, md, chains_dev, E, ws,
-                     cap, probs, status, lay, dbg, pe);
-  *err = hipGetLastError();
+  int dev = 0, cus = 0;
+  if ((*err = hipGetDevice(&dev)) != hipSuccess) return;
+  if ((*err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return;
+  const int per = cus / 2 > 0 ? cus / 2 : 1;
+  for (int c0 = 0; c0 < n_chains; c0 += per) {
+    const int nc = (n_chains - c0) < per ? (n_chains - c0) : per;
+    hipLaunchKernelGGL((sg_chain_kernel<KT, NB, PE>), dim3(2 * nc), dim3(NB), lds, s, md, chains_dev + c0, nc, E,
+                       ws, cap, probs, status + c0, lay, clay, dbg ? dbg + (size_t)16 * c0 : nullptr, pe);
+    if ((*err = hipGetLastError()) != hipSuccess) return;
+  }
 }
 // ------------------------------------------------------------- launches
 int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint16_t* meth, const uint16_t* tot,
@@ -1117,17 +1390,20 @@ int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint1
 
 
 int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
-                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* stream,
-                     const SgPeDev* pe) {
+                     const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* ctl,
+                     void* stream, const SgPeDev* pe) {
   if (n_chains <= 0) return HYG_OK;
   if (c.Nmax > kSgThreads || c.K < 2 || c.K > HYG_KMAX) return HYG_EUNSUPPORTED;
   const SgLay lay = sg_layout(c.K, psi_cap, pe != nullptr);
+  const SgCLay clay = sg_clayout(c.K, psi_cap);
+  const size_t lds = sg_lds_bytes(c, psi_cap, pe != nullptr);
   SgPeDev ped{};
   if (pe) ped = *pe;
-  if (lay.total > 160 * 1024) return HYG_EUNSUPPORTED;
+  if (lds > kSgLdsBudget) return HYG_EUNSUPPORTED;
   static const bool want_dbg = getenv("HYG_SG_PHASES") != nullptr;
   unsigned long long* dbg = nullptr;
   hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(ctl, 0, kSgCtlBytes * (size_t)n_chains, s) != hipSuccess) return HYG_EDEVICE;
   if (want_dbg && hipMalloc((void**)&dbg, sizeof(unsigned long long) * 16 * n_chains) != hipSuccess) dbg = nullptr;
   if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * 16 * n_chains, s);
   hipError_t err = hipErrorInvalidValue;
@@ -1136,10 +1412,10 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
   case k:                                                                                                        \
     if (pe)                                                                                                      \
       launch_chain_kt<k, (k <= 8 ? 512 : 256), true>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, \
-                                                     dbg, s, ped, &err);                                         \
+                                                     clay, lds, dbg, s, ped, &err);                              \
     else                                                                                                         \
       launch_chain_kt<k, (k <= 8 ? 512 : 256), false>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status,     \
-                                                      lay, dbg, s, ped, &err);                                   \
+                                                      lay, clay, lds, dbg, s, ped, &err);                        \
     break;
     SG_CASE(2) SG_CASE(3) SG_CASE(4) SG_CASE(5) SG_CASE(6) SG_CASE(7) SG_CASE(8) SG_CASE(9)
     SG_CASE(10) SG_CASE(11) SG_CASE(12) SG_CASE(13) SG_CASE(14) SG_CASE(15) SG_CASE(16)
@@ -1160,9 +1436,9 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
     for (int i = 1; i < n_chains; ++i)
       if (h[(size_t)i * 16 + 15] > h[(size_t)lc * 16 + 15]) lc = i;
     const double steps = (double)h[(size_t)lc * 16 + 15];
-    const char* nm[8] = {"copy", "sort", "kloop", "resample", "weights", "normalise", "smooth", "compact"};
-    fprintf(stderr, "[hyg sg phases] K=%d lds=%zu slots_lds=%d longest chain %d: %.0f steps, cycles/step:", c.K,
-            lay.total, lay.nl, lc, steps);
+    const char* nm[8] = {"copy", "sort", "kloop", "resample", "weights", "normalise", "record", "-"};
+    fprintf(stderr, "[hyg sg phases] K=%d lds=%zu smoothing slots_lds=%d longest chain %d: %.0f steps, cycles/step:",
+            c.K, lds, clay.nl, lc, steps);
     double sum = 0;
     for (int k = 0; k < 8; ++k) {
       const double v = (double)h[(size_t)lc * 16 + k] / steps;
