@@ -563,6 +563,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         uint64_t lkey = (tid < Np) ? sg_okey(plw) : 0;
         int lidx = tid;
         sg_bitonic<NB>(lkey, lidx, xk, xi);
+        if (!PE) { SG_PH(12); }
         const double* wP = w_ + pb * NT;
         if (fin > M) {
           // optimalFiniteState (resample.h:289-409) on the weights sorted
@@ -574,6 +575,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
           if (tid < NT) logq[tid] = q;
           lds_barrier();
           const bool mono = !block_or<NB>(tid + 1 < Np && logq[tid + 1] > q, red);
+          if (!PE) { SG_PH(13); }
           int idx = lidx;
           if (!mono) {
             uint64_t key = (tid < Np) ? sg_okey(pw) : 0;
@@ -593,6 +595,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
           }
           // reverse cumulative sums Q(k) = total - exclusive prefix (exact)
           block_scan128<NB>(mq, cum, red);
+          if (!PE) { SG_PH(14); }
           lds_barrier();
           {
             const hyg_u128 tot = cum[NB], ex = cum[tid];
@@ -1446,10 +1449,13 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
       sum += v;
     }
     const double pe_c = (double)h[(size_t)lc * 16 + 12] / steps, pe_r = (double)h[(size_t)lc * 16 + 13] / steps;
+    if (!pe)
+      fprintf(stderr, " [sort split: bitonic=%.0f gather+mono=%.0f log+scan=%.0f]", pe_c, pe_r,
+              (double)h[(size_t)lc * 16 + 14] / steps);
     if (pe)
       fprintf(stderr, " estimation=%.0f rebuild=%.0f (rows/rebuild %.0f)", pe_c, pe_r,
               (double)h[(size_t)lc * 16 + 14] / std::max(1.0, steps / (double)pe->c.every));
-    sum += pe_c + pe_r;
+    if (pe) sum += pe_c + pe_r;
     fprintf(stderr, " total=%.0f | optimal=%.0f keep_top=%.0f kloop_iters/capped=%.2f pending/step=%.2f\n", sum,
             (double)h[(size_t)lc * 16 + 8], (double)h[(size_t)lc * 16 + 9],
             (double)h[(size_t)lc * 16 + 10] /
