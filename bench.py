@@ -92,6 +92,29 @@ def host_cpus() -> dict:
     return info
 
 
+class _Heartbeat:
+    """Prints a progress line to stderr every `every` seconds while a long
+    host-side phase runs (a silent GPU job is taken to be hung)."""
+
+    def __init__(self, what: str, every: float = 30.0):
+        self.what, self.every = what, every
+        self._stop = threading.Event()
+
+    def __enter__(self):
+        def beat():
+            t0 = time.perf_counter()
+            while not self._stop.wait(self.every):
+                print(f"[bench] {self.what}: {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+        self._t = threading.Thread(target=beat, daemon=True)
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join()
+
+
 def _threads_run(fn, n):
     res = [None] * n
     th = [threading.Thread(target=lambda i=i: res.__setitem__(i, fn(i))) for i in range(n)]
@@ -132,12 +155,13 @@ def cpu_baseline(args, d_host, chains, seconds: float) -> dict:
         return ob.chain(p, E, 7 + i, i)["status"]
 
     out = {}
-    for name, fn, n_cal in (("reference_structure", refstruct, 200), ("optimised_port", port, 1500)):
-        t0 = time.perf_counter()
-        fn(0, n_cal)
-        per_site = (time.perf_counter() - t0) / n_cal
-        n_sites = int(max(500, min(100000, seconds / per_site)))
-        st, dt = _threads_run(lambda i: fn(i, n_sites), threads)
+    for name, fn, n_cal in (("reference_structure", refstruct, 40), ("optimised_port", port, 1500)):
+        with _Heartbeat(f"cpu baseline {name}"):
+            t0 = time.perf_counter()
+            fn(0, n_cal)
+            per_site = (time.perf_counter() - t0) / n_cal
+            n_sites = int(max(100, min(100000, seconds / per_site)))
+            st, dt = _threads_run(lambda i: fn(i, n_sites), threads)
         if any(s != 0 for s in st):
             raise RuntimeError(f"CPU baseline {name} failed: {st}")
         total = n_sites * threads

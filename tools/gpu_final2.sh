@@ -6,7 +6,6 @@ tag=$1
 O=gpurun_out/$tag
 mkdir -p $O
 run() { name=$1; shift; timeout -k 10 500 "$@" > $O/$name.log 2>&1 || { tail -5 $O/$name.log; exit 1; }; grep '^{' $O/$name.log | tail -1 | cut -c1-400; }
-run c4 python bench.py --job c4 --steps 1 --warmup 1 --no-cpu-baseline
 run c5 python bench.py --job c5 --steps 1 --warmup 1 --cpu-seconds 5
 run c2 python tools/bench_sg.py
 run c2pe python tools/bench_sg.py --estimate-parameters
