@@ -138,6 +138,27 @@ __device__ __forceinline__ hyg_u128 wave_sum128(hyg_u128 v) {
   return s;
 }
 
+// wave total of an exact u192 sum: quad / row mirrors, then the four row
+// results read out (fewer dependent steps than an inclusive scan)
+__device__ __forceinline__ hyg_u192 wave_sum192(hyg_u192 v) {
+  hyg_u192 w;
+  w.w0 = dpp64<kDppQuad1032>(v.w0); w.w1 = dpp64<kDppQuad1032>(v.w1); w.w2 = dpp64<kDppQuad1032>(v.w2);
+  v = hyg_u192_add(v, w);
+  w.w0 = dpp64<kDppQuad2301>(v.w0); w.w1 = dpp64<kDppQuad2301>(v.w1); w.w2 = dpp64<kDppQuad2301>(v.w2);
+  v = hyg_u192_add(v, w);
+  w.w0 = dpp64<kDppRowHalfMirror>(v.w0); w.w1 = dpp64<kDppRowHalfMirror>(v.w1); w.w2 = dpp64<kDppRowHalfMirror>(v.w2);
+  v = hyg_u192_add(v, w);
+  w.w0 = dpp64<kDppRowMirror>(v.w0); w.w1 = dpp64<kDppRowMirror>(v.w1); w.w2 = dpp64<kDppRowMirror>(v.w2);
+  v = hyg_u192_add(v, w);
+  hyg_u192 s = hyg_u192_zero();
+  for (int r = 0; r < 64; r += 16) {
+    hyg_u192 x;
+    x.w0 = rdlane64(v.w0, r); x.w1 = rdlane64(v.w1, r); x.w2 = rdlane64(v.w2, r);
+    s = hyg_u192_add(s, x);
+  }
+  return s;
+}
+
 // inclusive wave scans (Hillis-Steele inside rows, then row broadcasts)
 template <int CTRL, int RM>
 __device__ __forceinline__ hyg_u192 dpp192(hyg_u192 v) {

@@ -55,6 +55,83 @@ __device__ __forceinline__ int fdiv(int n, int d, float rd) {
   return q;
 }
 
+// hyg_fix100(hyg_exp(x[i])) for R values at once, written statement by
+// statement across the values: the same operations in the same order per
+// value as include/hyg_arith.h (so the same bits), but the R dependent f64
+// chains sit side by side in the instruction stream. Written as one function
+// per value, the compiler schedules the chains one after another and every
+// f64 operation waits for its predecessor's result.
+template <int R>
+__device__ __forceinline__ void exp_fix100_lockstep(const double (&x)[R], hyg_u128 (&out)[R]) {
+  double xc[R], kd[R], r[R], r2[R], r4[R], r8[R], p[R], v[R];
+  int k[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) xc[i] = __builtin_fmin(__builtin_fmax(x[i], -746.0), 710.0);
+#pragma unroll
+  for (int i = 0; i < R; ++i) kd[i] = __builtin_floor(xc[i] * HYG_INV_LN2 + 0.5);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    k[i] = (int)kd[i];
+    const double hi = xc[i] - kd[i] * HYG_LN2_HI;
+    const double lo = kd[i] * HYG_LN2_LO;
+    r[i] = hi - lo;
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) r2[i] = r[i] * r[i];
+#pragma unroll
+  for (int i = 0; i < R; ++i) r4[i] = r2[i] * r2[i];
+#pragma unroll
+  for (int i = 0; i < R; ++i) r8[i] = r4[i] * r4[i];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const double q0 = 1.0 + 1.0 * r[i];
+    const double q1 = 0.5 + 1.6666666666666665741e-01 * r[i];
+    const double q2 = 4.1666666666666664354e-02 + 8.3333333333333332177e-03 * r[i];
+    const double q3 = 1.3888888888888888889e-03 + 1.9841269841269841253e-04 * r[i];
+    const double q4 = 2.4801587301587301566e-05 + 2.7557319223985890653e-06 * r[i];
+    const double q5 = 2.7557319223985890653e-07 + 2.5052108385441718775e-08 * r[i];
+    const double q6 = 2.0876756987868098979e-09 + 1.6059043836821614599e-10 * r[i];
+    const double s0 = q0 + q1 * r2[i];
+    const double s1 = q2 + q3 * r2[i];
+    const double s2 = q4 + q5 * r2[i];
+    const double u0 = s0 + s1 * r4[i];
+    const double u1 = s2 + q6 * r4[i];
+    p[i] = u0 + u1 * r8[i];
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int big = k[i] > 1023, sub = k[i] < -1021;
+    const int k1 = big ? k[i] - 1 : (sub ? k[i] + 54 : k[i]);
+    const double p1 = big ? p[i] * 2.0 : p[i];
+    double w = p1 * hyg_pow2(k1);
+    w = sub ? w * 5.5511151231257827021e-17 : w;
+    w = (x[i] < -745.13321910194110842) ? 0.0 : w;
+    w = (x[i] > 709.782712893383973096) ? HYG_INF : w;
+    v[i] = (x[i] != x[i]) ? x[i] : w;
+  }
+  // hyg_fix100, statement by statement
+  double hf[R], lf[R], lhf[R], llf[R], hhf[R], hlf[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) v[i] = (v[i] > 0.0 && v[i] < 65536.0) ? v[i] * 0x1p100 : 0.0;
+#pragma unroll
+  for (int i = 0; i < R; ++i) hf[i] = __builtin_floor(v[i] * 0x1p-64);
+#pragma unroll
+  for (int i = 0; i < R; ++i) lf[i] = v[i] - hf[i] * 0x1p64;
+#pragma unroll
+  for (int i = 0; i < R; ++i) lhf[i] = __builtin_floor(lf[i] * 0x1p-32);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    llf[i] = lf[i] - lhf[i] * 0x1p32;
+    hhf[i] = __builtin_floor(hf[i] * 0x1p-32);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    hlf[i] = hf[i] - hhf[i] * 0x1p32;
+    out[i].lo = ((uint64_t)(uint32_t)lhf[i] << 32) | (uint64_t)(uint32_t)llf[i];
+    out[i].hi = ((uint64_t)(uint32_t)hhf[i] << 32) | (uint64_t)(uint32_t)hlf[i];
+  }
+}
+
 // --------------------------------------------------------------- model
 struct Hz4 {
   double lrc, l1c, lrk, l1k;  // log rho / log(1-rho) of control (d_c, r_c) and case (d_k, r_k)
@@ -244,11 +321,12 @@ __host__ __device__ inline int next_pow2(int x) {
 
 constexpr int kBuckets = 512;  // counting-sort buckets of the resampling sort (sqrt-spaced in -lw)
 constexpr int kNCut = 8;       // log-weight cutoffs of the top-set resampling path
+constexpr int kLR = 4;         // candidate-list entries per lane per chunk (lse / top-set gather)
 
-struct Lay {  // byte offsets into the dynamic LDS
-  size_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, rb, red, sh,
+struct Lay {  // byte offsets into the dynamic LDS (32-bit: one SGPR each in the kernels)
+  uint32_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, rb, red, sh,
       total;
-  size_t bcnt_bytes;
+  uint32_t bcnt_bytes;
   int npad, nkeys, nt;
   int topset_r;  // keys per lane of the top-set sort: A holds <= 64 * topset_r per wave
 };
@@ -820,8 +898,9 @@ enum { FAST_DONE = 0, FAST_FALLBACK = 1, FAST_FALLBACK_REGEN = 2 };
 // cutoffs of the top set in W - mx (nats below the largest weight); the last
 // set (k = kNCut - 1) is the whole candidate list (W - mx >= sig_thresh)
 __device__ __forceinline__ double cut_below_top(int k) {
-  constexpr double x[kNCut - 1] = {14.0, 17.0, 20.0, 23.0, 26.0, 30.0, 36.0};
-  return x[k];
+  // selects, not a table: a runtime index into a local array is a memory load
+  return k < 4 ? (k < 2 ? (k == 0 ? 14.0 : 17.0) : (k == 2 ? 20.0 : 23.0))
+               : (k < 6 ? (k == 4 ? 26.0 : 30.0) : 36.0);
 }
 
 // One compare-exchange stage (k, j) of a bitonic sort of 64*NW*R keys held
@@ -1003,42 +1082,64 @@ __device__ int top_set_resample(const double* W, int N, double mx, double logS, 
   constexpr int NW = NT / 64;
   const int wv = wave_id(), lane = lane_id();
   // ---- 1. the most inclusive cutoff whose set A fits the sort
-  int ks = -1, nA = 0, nL = 0;
-#pragma unroll
-  for (int k = 0; k < kNCut; ++k) {
-    int c = 0;
-    for (int w = 0; w < NW; ++w) c += part_cnt[w * kNCut + k];
-    const int np = (c <= 64 * NW) ? 64 * NW : 128 * NW;
-    if (c <= 64 * NW * rmax && (size_t)np * sizeof(hyg_u192) <= scr_bytes && (size_t)np * 8 <= srt_bytes) {
-      ks = k;
-      nA = c;
-    }
-    nL = c;
-  }
+  // one LDS read per lane (lane w * kNCut + k holds wave w's count at cutoff
+  // k), the per-cutoff totals by xor shuffles (every lane l gets cutoff l % 8)
+  static_assert(kNCut == 8 && NW * kNCut <= 64, "cutoff counts: one per lane");
+  const int pc = (lane < NW * kNCut) ? part_cnt[lane] : 0;
+  int c = pc;
+  c += (int)xshfl32<8>((uint32_t)c);
+  c += (int)xshfl32<16>((uint32_t)c);
+  c += (int)xshfl32<32>((uint32_t)c);
+  const int np = (c <= 64 * NW) ? 64 * NW : 128 * NW;
+  const bool fits = lane < kNCut && c <= 64 * NW * rmax && (size_t)np * sizeof(hyg_u192) <= scr_bytes &&
+                    (size_t)np * 8 <= srt_bytes;
+  const uint64_t fm = wave_ballot(fits);
+  const int nL = __builtin_amdgcn_readlane(c, kNCut - 1);
   if (threadIdx.x == 0) sh.n_sig = nL;
-  if (ks < 0) return FAST_FALLBACK;  // uniform
+  if (fm == 0) return FAST_FALLBACK;  // uniform
+  const int ks = 63 - __builtin_clzll(fm);  // the most inclusive cutoff that fits
+  const int nA = __builtin_amdgcn_readlane(c, ks);
   const bool hasB = nA < nL;         // list weights outside A (their masses enter the total)
   const double cutx = (ks == kNCut - 1) ? HYG_NINF : -cut_below_top(ks);
   int off = 0;
-  for (int w = 0; w < wv; ++w) off += part_cnt[w * kNCut + ks];
+  for (int w = 0; w < wv; ++w) off += __builtin_amdgcn_readlane(pc, w * kNCut + ks);
   // ---- 2. gather A's keys; exact mass of the list weights outside A
-  hyg_u192 mb = hyg_u192_zero();
-  for (int i = 0; i < cw; i += 64) {
-    const bool v = i + lane < cw;
-    const int n = lst[lb + (v ? i + lane : cw - 1)];
-    const double x = W[n] - mx;
-    const float lw = (float)(x - logS);
-    const bool inA = v && x >= cutx;
-    const uint64_t bal = wave_ballot(inA);
-    if (inA) srt[off + lanes_below(bal)] = sort_key(lw, n);
-    off += (int)__builtin_popcountll(bal);
+  hyg_u192 mb = hyg_u192_zero(), mb2 = hyg_u192_zero();
+  for (int b = 0; b < cw; b += 64 * kLR) {  // kLR entries per lane, loads first (see the lse loop)
+    int nn[kLR];
+    float lw[kLR];
+    bool inA[kLR], outA[kLR];
+#pragma unroll
+    for (int r = 0; r < kLR; ++r) {
+      const int i = b + r * 64 + lane;
+      nn[r] = lst[lb + (i < cw ? i : b)];
+    }
+#pragma unroll
+    for (int r = 0; r < kLR; ++r) {
+      const bool v = b + r * 64 + lane < cw;
+      const double x = W[nn[r]] - mx;
+      lw[r] = (float)(x - logS);
+      inA[r] = v && x >= cutx;
+      outA[r] = v && !inA[r];
+    }
+#pragma unroll
+    for (int r = 0; r < kLR; ++r) {
+      const uint64_t bal = wave_ballot(inA[r]);
+      if (inA[r]) srt[off + lanes_below(bal)] = sort_key(lw[r], nn[r]);
+      off += (int)__builtin_popcountll(bal);
+    }
     if (hasB) {  // uniform; expf(lw) is 0 below sig_thresh
-      const float m = hyg_expf(lw);
-      mb = hyg_u192_add(mb, hyg_fix149f((v && !inA) ? m : 0.0f));
+#pragma unroll
+      for (int r = 0; r < kLR; ++r) {
+        const float m = hyg_expf(lw[r]);
+        const hyg_u192 f = hyg_fix149f(outA[r] ? m : 0.0f);
+        if (r & 1) mb2 = hyg_u192_add(mb2, f); else mb = hyg_u192_add(mb, f);
+      }
     }
   }
+  mb = hyg_u192_add(mb, mb2);
   if (hasB) {
-    const hyg_u192 ws = rdlane192(wave_incl192(mb), 63);
+    const hyg_u192 ws = wave_sum192(mb);
     if (lane == 0) part_tot[wv] = ws;
   }
   lds_barrier();
@@ -1095,6 +1196,10 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
                   double* __restrict__ finalw_out, Lay lay, unsigned long long* __restrict__ dbg) {
   const hyg_tg_consts* __restrict__ c = md.consts;
   const int K = c->K, M = c->M, I = c->I, K2 = 2 * K, tid = threadIdx.x;
+  // in a register for the whole chain: a load of c-> inside the step loop is a
+  // global load the compiler cannot hoist past the record stores (it may
+  // alias them), followed by a vmcnt(0) wait on every outstanding store
+  const float sig_thresh = c->sig_thresh;
   const ChainDev ch = chains[blockIdx.x];
   const int T = ch.T;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -1172,46 +1277,70 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     int lst_cnt = 0;
     const bool topset = cnt > M && M <= 64;  // this step resamples by the top-set path
     {
-      const double cutw = (double)c->sig_thresh;
-      for (int b = wave_id() * 64; b < N; b += NT) {
-        const int n = b + lane_id();
-        const bool keep = (n < N) && (W[n] - mx >= cutw);
-        const uint64_t bal = wave_ballot(keep);
-        if (keep) lst[lst_base + lst_cnt + lanes_below(bal)] = n;
-        lst_cnt += (int)__builtin_popcountll(bal);
+      // kCC candidates per lane at a time, their loads issued together (a
+      // load / compare / ballot per iteration waits out an LDS round trip each)
+      const double cutw = (double)sig_thresh;
+      constexpr int kCC = 8;
+      for (int b0 = wave_id() * 64; b0 < N; b0 += kCC * NT) {
+        bool keep[kCC];
+#pragma unroll
+        for (int j = 0; j < kCC; ++j) {
+          const int n = b0 + j * NT + lane_id();
+          const double w = W[n < N ? n : 0];
+          // `&`, not `&&`: a short-circuit test puts the load under a branch
+          // and waits out its round trip before the next candidate's load
+          keep[j] = (n < N) & (w - mx >= cutw);
+        }
+#pragma unroll
+        for (int j = 0; j < kCC; ++j) {
+          const uint64_t bal = wave_ballot(keep[j]);
+          if (keep[j]) lst[lst_base + lst_cnt + lanes_below(bal)] = b0 + j * NT + lane_id();
+          lst_cnt += (int)__builtin_popcountll(bal);
+        }
       }
       wave_lds_sync();
     }
+    PH(22);
     double logS;
     {
-      // two independent chains per iteration; fix100(exp(x)) is 0 for x < -70.
+      // kLR list entries per lane at a time: every load of the chunk issued
+      // first, then kLR independent exp / fixed-point chains in straight-line
+      // code (hyg_fix100 is branch-free), so they interleave. fix100(exp(x))
+      // is 0 for x < -70; padding lanes take x = -inf (mass 0, no cutoff).
       // Top-set steps also count the list per cutoff (per-lane counters).
       hyg_u128 s0 = hyg_u128_zero(), s1 = hyg_u128_zero();
       int ccut[kNCut - 1];
 #pragma unroll
       for (int k = 0; k < kNCut - 1; ++k) ccut[k] = 0;
-      int i = lane_id();
-      for (; i + 64 < lst_cnt; i += 128) {
-        const double x0 = W[lst[lst_base + i]] - mx, x1 = W[lst[lst_base + i + 64]] - mx;
-        s0 = hyg_u128_add(s0, hyg_fix100(hyg_exp(x0)));
-        s1 = hyg_u128_add(s1, hyg_fix100(hyg_exp(x1)));
-        if (topset) {
+      for (int b = 0; b < lst_cnt; b += 64 * kLR) {  // lst_cnt is wave-uniform
+        int nn[kLR];
+        double xx[kLR];
 #pragma unroll
-          for (int k = 0; k < kNCut - 1; ++k)
-            ccut[k] += ((x0 >= -cut_below_top(k)) ? 1 : 0) + ((x1 >= -cut_below_top(k)) ? 1 : 0);
+        for (int r = 0; r < kLR; ++r) {
+          const int i = b + r * 64 + lane_id();
+          nn[r] = lst[lst_base + (i < lst_cnt ? i : b)];
+        }
+#pragma unroll
+        for (int r = 0; r < kLR; ++r) {
+          const double w = W[nn[r]];
+          xx[r] = (b + r * 64 + lane_id() < lst_cnt) ? w - mx : HYG_NINF;
+        }
+        hyg_u128 ff[kLR];
+        exp_fix100_lockstep<kLR>(xx, ff);
+#pragma unroll
+        for (int r = 0; r < kLR; ++r) {
+          if (r & 1) s1 = hyg_u128_add(s1, ff[r]); else s0 = hyg_u128_add(s0, ff[r]);
+        }
+        if (topset) {  // wave counts per cutoff by ballots (scalar sums)
+#pragma unroll
+          for (int r = 0; r < kLR; ++r)
+#pragma unroll
+            for (int k = 0; k < kNCut - 1; ++k)
+              ccut[k] += (int)__builtin_popcountll(wave_ballot(xx[r] >= -cut_below_top(k)));
         }
       }
-      if (i < lst_cnt) {
-        const double x0 = W[lst[lst_base + i]] - mx;
-        s0 = hyg_u128_add(s0, hyg_fix100(hyg_exp(x0)));
-        if (topset) {
-#pragma unroll
-          for (int k = 0; k < kNCut - 1; ++k) ccut[k] += (x0 >= -cut_below_top(k)) ? 1 : 0;
-        }
-      }
+      PH(23);
       if (topset) {
-#pragma unroll
-        for (int k = 0; k < kNCut - 1; ++k) ccut[k] = wave_sum(ccut[k]);
         if (lane_id() == 0) {  // read after the reduction's barriers below
 #pragma unroll
           for (int k = 0; k < kNCut - 1; ++k) part_cnt[wave_id() * kNCut + k] = ccut[k];
@@ -1265,7 +1394,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
           }
           lds_barrier();
         }
-        optimal_resample<NT>(W, (uint64_t*)W, N, mx, logS, c->sig_thresh, keys, bcnt, bpos, pre64, tau, parents,
+        optimal_resample<NT>(W, (uint64_t*)W, N, mx, logS, sig_thresh, keys, bcnt, bpos, pre64, tau, parents,
                              sh, cl, red, M, cnt, ch.seed, ch.chain_id, t, Ucur, ph_acc, dbg != nullptr);
         if (dbg && tid == 0) ph_acc[21]++;
       }
@@ -1508,6 +1637,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
                    unsigned long long* __restrict__ dbg) {
   const hyg_tg_consts* __restrict__ c = md.consts;
   const int K = c->K, M = c->M, B = c->B, I = c->I, K2 = 2 * K, tid = threadIdx.x;
+  const int Nmax = c->Nmax;  // hoisted: see sig_thresh in tg_forward_kernel
   const ChainDev ch = chains[blockIdx.x];
   const int T = ch.T;
   if (status_in[blockIdx.x] != HYG_OK) return;  // uniform
@@ -1593,7 +1723,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     // The rows of the backward kernel need the weights of the few candidates
     // that can reach a trajectory's next state only; all N weights are built
     // for the final step's draw and for the general paths.
-    const bool fast = (s.mode != MODE_INIT) && np <= 64 && B <= 64 && c->Nmax >= 192 && t != T - 1;
+    const bool fast = (s.mode != MODE_INIT) && np <= 64 && B <= 64 && Nmax >= 192 && t != T - 1;
     bool w_ready = false;
     auto make_W = [&]() {
       if (s.mode == MODE_INIT) gen_weights_init<NT>(cl, K, s.r_ph, Et, W, &mloc, &cloc);
@@ -1715,7 +1845,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         lds_barrier();
         int* lst_n = (int*)cp128;  // list indices (cp area, NT+1 u128 = 4(NT+1) ints)
         double* lst_l = Lg;        // list logits
-        const int cap = (4 * (NT + 1) < c->Nmax) ? 4 * (NT + 1) : c->Nmax;
+        const int cap = (4 * (NT + 1) < Nmax) ? 4 * (NT + 1) : Nmax;
         if (!fast) {
           for (int n = tid; n < N; n += NT) {
             const double w = W[n];
@@ -1784,7 +1914,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         };
         if (pre_bits && g == 0 && t >= 1 && wave_id() == NT / 64 - 1)  // next step's bits, while wave 0 draws
           backward_bits(rb + ((t - 1) & 1) * rbs, B, t - 1, ch.seed, ch.chain_id);
-        if (L <= 64 && B <= 64 && c->Nmax >= 192) {
+        if (L <= 64 && B <= 64 && Nmax >= 192) {
           // ---- one wave: order the list by n, exact masses, scan, draws
           if (wave_id() == 0) {
             const int lane = lane_id();
@@ -1938,17 +2068,24 @@ void ev_record(int k, bool end, hipStream_t s) {
   (void)hipEventRecord(e, s);
   g_ev_used[k] = true;
 }
-// Threads per chain workgroup (HYG_THREADS, or HYG_THREADS_FWD / _BWD per kernel).
-int threads_per_chain(bool backward) {
-  static int nt[2] = {0, 0};
+// Threads per chain workgroup: HYG_THREADS (or HYG_THREADS_FWD / _BWD) if set;
+// otherwise 256, or 512 when the forward's LDS at 256 threads already forces one
+// workgroup per CU (K = 12, C5: 145 KB): the CU then holds one chain either
+// way, and twice the waves halve each thread's share of the N = M (2K + K^2)
+// candidates (C5: 5.67 M -> 6.52 M site-seeds/s).
+int threads_per_chain(bool backward, const hyg_tg_consts& c) {
+  static int env[2] = {-1, -1};
   const int k = backward ? 1 : 0;
-  if (!nt[k]) {
+  if (env[k] < 0) {
     const char* v = getenv(backward ? "HYG_THREADS_BWD" : "HYG_THREADS_FWD");
     if (!v) v = getenv("HYG_THREADS");
-    const int x = v ? atoi(v) : (backward ? kDefaultThreadsBwd : kDefaultThreads);
-    nt[k] = (x == 64 || x == 128 || x == 256 || x == 512) ? x : kDefaultThreads;
+    const int x = v ? atoi(v) : 0;
+    env[k] = (x == 64 || x == 128 || x == 256 || x == 512) ? x : 0;
   }
-  return nt[k];
+  if (env[k]) return env[k];
+  const int def = backward ? kDefaultThreadsBwd : kDefaultThreads;
+  const size_t lds = make_layout(c.K, c.M, c.B, c.Nmax, def, false).total;
+  return (2 * lds > 160 * 1024) ? 512 : def;
 }
 }  // namespace
 
@@ -1967,10 +2104,10 @@ int last_kernel_ms(float* out3) {
 }
 
 size_t forward_lds_bytes(const hyg_tg_consts& c) {
-  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(false), false).total;
+  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(false, c), false).total;
 }
 size_t backward_lds_bytes(const hyg_tg_consts& c) {
-  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(true), true).total;
+  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(true, c), true).total;
 }
 
 int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* meth_c, const uint16_t* tot_c,
@@ -2024,7 +2161,8 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
     }
     fprintf(stderr, " total=%.0f | keep_steps=%.0f mean_nsig=%.1f mean_n2=%.1f", sum, (double)tot[10],
             tot[9] / (steps - tot[10]), 0.0);
-    fprintf(stderr, " | lse loop=%.0f lse reduce=%.0f", tot[12] / steps, tot[11] / steps);
+    fprintf(stderr, " | list=%.0f lse loop=%.0f cut sums=%.0f lse reduce=%.0f", tot[22] / steps, tot[23] / steps,
+            tot[12] / steps, tot[11] / steps);
     const double opt = steps - tot[10];
     fprintf(stderr, " | topset: compact=%.0f mass=%.0f gatherA=%.0f sort=%.0f prefix=%.0f kloop_sys=%.0f",
             tot[24] / opt, tot[25] / opt, tot[26] / opt, tot[27] / opt, tot[28] / opt, tot[29] / opt);
@@ -2082,14 +2220,14 @@ int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* ch
   if (n_chains <= 0) return HYG_OK;
   hipStream_t s = (hipStream_t)stream;
   int rc;
-  switch (threads_per_chain(false)) {
+  switch (threads_per_chain(false, c)) {
     case 64: rc = launch_forward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     case 128: rc = launch_forward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     case 256: rc = launch_forward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     default: rc = launch_forward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s); break;
   }
   if (rc != HYG_OK) return rc;
-  switch (threads_per_chain(true)) {
+  switch (threads_per_chain(true, c)) {
     case 64: return launch_backward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s);
     case 128: return launch_backward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s);
     case 256: return launch_backward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s);

@@ -162,9 +162,36 @@ HYG_HD double hyg_log(double x) {
   return (x != x || x < 0.0) ? HYG_NAN : v;
 }
 
-/* f32 versions used where the reference computes in float32
- * (resampling_functions.py:7-68): evaluated in double, rounded once. */
-HYG_HD float hyg_expf(float x) { return (float)hyg_exp((double)x); }
+/* exp(x) for float x in float32 arithmetic only, ~1 ulp: the resampling
+ * masses (resampling_functions.py:10,59 take tf.exp of the float32
+ * log-weights). Cody-Waite reduction x = k ln2 + r (ln2_hi has 15 significant
+ * bits, so k*ln2_hi is exact for |k| <= 150), the degree-7 Taylor polynomial of
+ * e^r (|r| <= 0.347, truncation < 0.05 ulp) by Estrin's scheme, then a scale
+ * by 2^k in one product (normal results; two products, the first exact, for
+ * subnormal ones; k > 127: (2p) 2^(k-1)), every step an IEEE f32 basic
+ * operation, so host and device give the same bits. */
+HYG_HD float hyg_expf(float x) {
+  const float xc = (float)HYG_FMIN(HYG_FMAX((double)x, -104.0), 89.0); /* NaN -> -104 */
+  const float kf = (float)HYG_FLOOR((double)(xc * 0x1.715476p+0f + 0.5f));
+  const float hi = xc - kf * 0x1.62e4p-1f;
+  const float r = hi - kf * 0x1.7f7d1cp-20f;
+  const float r2 = r * r;
+  const float r4 = r2 * r2;
+  const float q0 = 1.0f + r;
+  const float q1 = 0.5f + 0x1.555556p-3f * r;           /* 1/2!, 1/3! */
+  const float q2 = 0x1.555556p-5f + 0x1.111112p-7f * r; /* 1/4!, 1/5! */
+  const float q3 = 0x1.6c16c2p-10f + 0x1.a01a02p-13f * r; /* 1/6!, 1/7! */
+  const float p = (q0 + q1 * r2) + (q2 + q3 * r2) * r4;
+  const int k = (int)kf;
+  const int big = k > 127, sub = k < -126;
+  const int k1 = big ? k - 1 : (sub ? k + 64 : k);
+  const float p1 = big ? p * 2.0f : p;
+  float v = p1 * hyg_bits_f32((uint32_t)(k1 + 127) << 23);
+  v = sub ? v * 0x1p-64f : v;
+  v = (x < -104.0f) ? 0.0f : v;
+  v = (x > 89.0f) ? hyg_bits_f32(0x7f800000u) : v;
+  return (x != x) ? x : v;
+}
 HYG_HD float hyg_logf(float x) { return (float)hyg_log((double)x); }
 
 /* ------------------------------------------------------ 64-bit integer help */
@@ -187,23 +214,24 @@ HYG_HD hyg_u128 hyg_u128_add(hyg_u128 a, hyg_u128 b) {
 HYG_HD int hyg_u128_lt(hyg_u128 a, hyg_u128 b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
 HYG_HD int hyg_u128_is_zero(hyg_u128 a) { return (a.lo | a.hi) == 0; }
 
-/* floor(e * 2^100) for e in [0, 1]; masses below 2^-100 become 0.
- * Branch-free (selects only), so unrolled GPU loops can interleave. */
+/* floor(e * 2^100) for e in [0, 2^16) (masses are in [0, 1]); masses below
+ * 2^-100, non-positive or NaN e, and e >= 2^16 give 0. Computed in f64 basic
+ * operations, every step exact: v = e 2^100 (a power-of-two scaling), its
+ * 32-bit limbs by floor and exact differences (v - floor(v / 2^64) 2^64 is v
+ * mod 2^64, which has at most 53 significant bits), the last limb truncated
+ * by the conversion. No shifts and no branches, so unrolled GPU loops
+ * interleave independent masses. */
 HYG_HD hyg_u128 hyg_fix100(double e) {
-  const uint64_t b = hyg_f64_bits(e);
-  const int E = (int)((b >> 52) & 0x7ff);
-  const uint64_t mant = (b & 0x000fffffffffffffull) | 0x0010000000000000ull;
-  const int sh = E - 975; /* value*2^100 = mant * 2^(E-1075+100); sh <= 48 for e <= 1 */
-  const int shp = (sh > 0 ? sh : 0) & 63, shn = (sh < 0 ? -sh : 0) & 63;
-  const uint64_t up_lo = mant << shp;
-  const uint64_t up_hi = (mant >> 1) >> (63 - shp); /* mant >> (64 - shp), 0 for shp = 0 */
-  const uint64_t dn_lo = mant >> shn;
+  const double v = (e > 0.0 && e < 65536.0) ? e * 0x1p100 : 0.0;
+  const double hf = HYG_FLOOR(v * 0x1p-64);  /* < 2^52 */
+  const double lf = v - hf * 0x1p64;         /* [0, 2^64) */
+  const double lhf = HYG_FLOOR(lf * 0x1p-32); /* [0, 2^32) */
+  const double llf = lf - lhf * 0x1p32;       /* [0, 2^32), fractional below 2^52 */
+  const double hhf = HYG_FLOOR(hf * 0x1p-32);
+  const double hlf = hf - hhf * 0x1p32;
   hyg_u128 r;
-  r.lo = (sh >= 0) ? up_lo : ((sh > -64) ? dn_lo : 0);
-  r.hi = (sh > 0) ? up_hi : 0;
-  const int zero = !(e > 0.0) || E == 0 || sh >= 64;
-  r.lo = zero ? 0 : r.lo;
-  r.hi = zero ? 0 : r.hi;
+  r.lo = ((uint64_t)(uint32_t)lhf << 32) | (uint64_t)(uint32_t)llf;
+  r.hi = ((uint64_t)(uint32_t)hhf << 32) | (uint64_t)(uint32_t)hlf;
   return r;
 }
 

@@ -119,6 +119,10 @@ def lib() -> C.CDLL:
         L.oracle_exp.argtypes = [d]
         L.oracle_log.restype = d
         L.oracle_log.argtypes = [d]
+        L.oracle_expf.restype = C.c_float
+        L.oracle_expf.argtypes = [C.c_float]
+        L.oracle_fix100.restype = None
+        L.oracle_fix100.argtypes = [d, C.POINTER(C.c_uint64)]
         L.oracle_philox.restype = None
         L.oracle_philox.argtypes = [u64] * 6 + [vp]
         L.oracle_u192_roundtrip.restype = d

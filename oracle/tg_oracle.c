@@ -588,6 +588,8 @@ int oracle_tg_consts(const hyg_tg_params* p, hyg_tg_consts* out) { return hyg_tg
 /* arithmetic primitives for tests/test_arith.py */
 double oracle_exp(double x) { return hyg_exp(x); }
 double oracle_log(double x) { return hyg_log(x); }
+float oracle_expf(float x) { return hyg_expf(x); }
+void oracle_fix100(double e, uint64_t* out2) { const hyg_u128 v = hyg_fix100(e); out2[0] = v.lo; out2[1] = v.hi; }
 void oracle_philox(uint64_t c0, uint64_t c1, uint64_t c2, uint64_t c3, uint64_t k0, uint64_t k1, uint64_t* out) {
   const hyg_ph4 r = hyg_philox4x64(c0, c1, c2, c3, k0, k1);
   for (int i = 0; i < 4; ++i) out[i] = r.v[i];

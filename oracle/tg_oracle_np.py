@@ -119,8 +119,39 @@ def f32(x) -> np.float32:
     return np.float32(x)
 
 
+_F = lambda h: np.float32(float.fromhex(h))  # noqa: E731
+_EXPF_C = {k: _F(v) for k, v in dict(log2e="0x1.715476p+0", hi="0x1.62e4p-1", lo="0x1.7f7d1cp-20",
+                                      c3="0x1.555556p-3", c4="0x1.555556p-5", c5="0x1.111112p-7",
+                                      c6="0x1.6c16c2p-10", c7="0x1.a01a02p-13").items()}
+
+
 def det_expf(x: np.float32) -> np.float32:
-    return np.float32(det_exp(float(x)))
+    """hyg_expf: exp in float32 basic operations (Cody-Waite + degree-7 Taylor,
+    Estrin), the same operations in the same order as include/hyg_arith.h."""
+    x = np.float32(x)
+    if x != x:
+        return x
+    if x < np.float32(-104.0):
+        return np.float32(0.0)
+    if x > np.float32(89.0):
+        return np.float32(np.inf)
+    c = _EXPF_C
+    one, half = np.float32(1.0), np.float32(0.5)
+    kf = np.float32(math.floor(float(x * c["log2e"] + half)))
+    r = (x - kf * c["hi"]) - kf * c["lo"]
+    r2 = r * r
+    r4 = r2 * r2
+    q0 = one + r
+    q1 = half + c["c3"] * r
+    q2 = c["c4"] + c["c5"] * r
+    q3 = c["c6"] + c["c7"] * r
+    p = (q0 + q1 * r2) + (q2 + q3 * r2) * r4
+    k = int(kf)
+    if k > 127:
+        return p * np.float32(2.0) * np.float32(2.0 ** (k - 1))
+    if k < -126:
+        return (p * np.float32(2.0 ** (k + 64))) * np.float32(2.0 ** -64)
+    return p * np.float32(2.0 ** k)
 
 
 def det_logf(x: np.float32) -> np.float32:
@@ -128,8 +159,8 @@ def det_logf(x: np.float32) -> np.float32:
 
 
 def fix100(e: float) -> int:
-    """floor(e * 2^100) exactly."""
-    if not e > 0.0:
+    """floor(e * 2^100) exactly (0 for e <= 0, NaN and e >= 2^16, as hyg_fix100)."""
+    if not 0.0 < e < 65536.0:
         return 0
     m, ex = math.frexp(e)  # e = m 2^ex, m in [0.5,1): mant = m*2^53
     mant = int(m * (1 << 53))

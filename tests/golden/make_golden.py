@@ -18,7 +18,8 @@ Fixtures (npz, inputs + expected outputs):
 
 The single-group oracle is pinned by tests/test_sg_oracle.py (exact semi-Markov
 smoother without resampling, scipy tables).
-``python tests/golden/make_golden.py sg`` regenerates only the sg_* fixtures.
+``python tests/golden/make_golden.py sg`` regenerates only the sg_* fixtures, ``... tg`` only
+the two-group chains.
 """
 from __future__ import annotations
 
@@ -124,6 +125,8 @@ def main():
     if not only_sg:
         for name, kw in CHAINS.items():
             chain_fixture(name, **kw)
+        if "tg" in sys.argv[1:]:  # the two-group chains only
+            return
         tables_fixture()
     for name, kw in SG_CHAINS.items():
         sg_chain_fixture(name, **kw)

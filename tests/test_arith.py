@@ -38,6 +38,32 @@ def test_exp_accuracy_and_python_restatement(oracle):
     assert math.isnan(L.oracle_exp(float("nan")))
 
 
+def test_expf_accuracy_and_python_restatement(oracle):
+    """hyg_expf (float32 arithmetic): within 2 f32 ulp of the correctly rounded
+    exp over the log-weight range, exact 0 below the subnormal range, and the
+    same bits as the numpy-float32 restatement."""
+    L = oracle.lib()
+    rng = np.random.default_rng(5)
+    xs = np.concatenate([rng.uniform(-104.5, 0, 6000), rng.uniform(-1, 1, 2000), rng.uniform(-88, 88.7, 1000),
+                         [0.0, -0.0, 1.0, -1.0, -87.3, -87.34, -100.0, -103.27, -103.3, -103.97, -104.0, -104.1,
+                          88.72, 88.73, 89.5]]).astype(np.float32)
+    worst = 0
+    for x in xs:
+        v = np.float32(L.oracle_expf(C.c_float(x)))
+        p = onp.det_expf(x)
+        assert v.view(np.uint32) == np.float32(p).view(np.uint32), (x, v, p)
+        ref = np.float32(math.exp(float(x))) if float(x) < 88.72283935546875 else np.float32(np.inf)
+        if np.isfinite(ref):
+            # ulps in the f32 grid (subnormals included: the bit patterns are consecutive)
+            worst = max(worst, abs(int(v.view(np.int32)) - int(ref.view(np.int32))))
+        else:
+            assert v == np.inf
+    assert worst <= 2, worst
+    assert L.oracle_expf(C.c_float(-110.0)) == 0.0
+    assert L.oracle_expf(C.c_float(float("-inf"))) == 0.0
+    assert math.isnan(L.oracle_expf(C.c_float(float("nan"))))
+
+
 def test_log_accuracy_and_python_restatement(oracle):
     L = oracle.lib()
     rng = np.random.default_rng(2)
@@ -84,6 +110,13 @@ def test_fixed_point_roundtrips(oracle):
         assert v == onp.int_to_f64(onp.fix100(float(e)), 100)
         assert abs(v - e) <= max(e * 2.0 ** -52, 2.0 ** -100)  # truncation of floor(e 2^100)
     assert L.oracle_u128_roundtrip(2.0 ** -101) == 0.0
+    # the limbs themselves, exactly (Python ints)
+    out = (C.c_uint64 * 2)()
+    edge = [0.0, -0.0, -1.0, 1.0, 2.0 ** -100, 2.0 ** -101, 2.0 ** -100 * 1.5, 5e-324, 2.0 ** -52, 0.5,
+            1.0 - 2.0 ** -53, 3.75, 65535.99, 65536.0, float("inf"), float("nan")]
+    for e in list(es) + list(rng.uniform(0, 2.0 ** -60, 500)) + edge:
+        L.oracle_fix100(float(e), out)
+        assert (out[1] << 64) | out[0] == onp.fix100(float(e)), e
 
 
 @pytest.mark.parametrize("T", [0.0, 1.0, 0.5, 1e-45, 3.3e-39, 0.999999940395, 0.123456789])
