@@ -230,6 +230,8 @@ def main():
     ap.add_argument("--history-gib", type=float, default=100.0, help="forward->backward history budget in HBM")
     ap.add_argument("--launch-chains", type=int, default=768, help="chains per launch when over the budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm); gloo rehearses the multi-rank path, e.g. 2 ranks on one GPU")
     args = ap.parse_args()
     preset = {"c3": (2, 4, 6), "c4": (None, 4, 6), "c5": (4, 50, 12)}[args.job]
     args.seeds = args.seeds if args.seeds is not None else preset[0]
@@ -245,9 +247,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local if world > 1 else 0)
+        # (local % device count: a gloo rehearsal may put several ranks on one GPU)
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", local % torch.cuda.device_count() if world > 1 else 0)
     torch.cuda.set_device(dev)
 
     from hygeia_amd import _lib, parallel, synthetic, two_group

@@ -143,10 +143,11 @@ def load() -> C.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("HYG_LIB_PATH", LIB_PATH)  # A/B builds of the same sources (tools/)
+    if path == LIB_PATH and not os.path.exists(LIB_PATH):
         from . import build as _build
         _build.build()
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp, i32, i64, u64, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_size_t
     L.hyg_tg_params_default.restype = None
     L.hyg_tg_params_default.argtypes = [C.POINTER(TgParams)]
