@@ -624,7 +624,7 @@ __device__ __forceinline__ void categorical_block(int N, double lmax, LogitFn lo
 // Writes parents[0..M) and sh.Kk / sh.log_c (log_c not finite -> caller
 // runs the unbiased fallback). Returns n_sig via sh.n_sig.
 template <int NT>
-__device__ void optimal_resample(const double* W, uint64_t* sorted, int N, double mx, double logS, float thr,
+__device__ __forceinline__ void optimal_resample(const double* W, uint64_t* sorted, int N, double mx, double logS, float thr,
                                  uint64_t* keys, int* bcnt, int* bpos, hyg_u192* pre64, hyg_u192* tau, int* parents,
                                  Shared& sh,
                                  const ConstLds& cl, unsigned char* red, int M, int cnt_fin, uint64_t seed,
@@ -959,7 +959,7 @@ struct Bitonic {
 // Sort A (nA keys in srt[]), exact prefix masses, the K / log c loop and the
 // systematic draws. scr: the W + key areas (W is overwritten).
 template <int NT, int R>
-__device__ int top_set_finish(uint64_t* srt, int nA, bool hasB, int N, int M, int cnt_fin, const hyg_u192& massB,
+__device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, int N, int M, int cnt_fin, const hyg_u192& massB,
                               unsigned char* scr, int* parents, Shared& sh, const ConstLds& cl, unsigned char* red,
                               float Usys, unsigned long long* ph, bool timed) {
   const int lane = lane_id();
@@ -1074,7 +1074,7 @@ __device__ int top_set_finish(uint64_t* srt, int nA, bool hasB, int N, int M, in
 // counts of the cutoff sets per wave (part_cnt) were published with the
 // candidate lists before the log-sum-exp reduction.
 template <int NT>
-__device__ int top_set_resample(const double* W, int N, double mx, double logS, const int* lst, int lb, int cw,
+__device__ __forceinline__ int top_set_resample(const double* W, int N, double mx, double logS, const int* lst, int lb, int cw,
                                 unsigned char* scr, size_t scr_bytes, uint64_t* srt, size_t srt_bytes,
                                 const int* part_cnt, hyg_u192* part_tot, int* parents, Shared& sh,
                                 const ConstLds& cl, unsigned char* red, int M, int cnt_fin, float Usys,
@@ -1188,14 +1188,20 @@ tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
   }
 }
 
-// 3 workgroups per CU at NT = 256 (<= 168 VGPRs): all C3 chains resident at once
-template <int NT>
+// 3 workgroups per CU at NT = 256 (<= 168 VGPRs): all C3 chains resident at once.
+// KC/MC/BC > 0: an instantiation for one model shape (the pipeline's K = 6,
+// M = 50, B = 25): K, M, B, the candidate count and the whole LDS layout are
+// then compile-time constants (LDS addresses fold into instruction offsets,
+// loops over slots get constant trip counts); KC = 0 reads them at run time.
+template <int NT, int KC = 0, int MC = 0, int BC = 0>
 __global__ void __launch_bounds__(NT, (NT <= 256 ? 3 : 1))
 tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                   uint8_t* __restrict__ ws, int32_t* status_out, double* __restrict__ logz_out,
-                  double* __restrict__ finalw_out, Lay lay, unsigned long long* __restrict__ dbg) {
+                  double* __restrict__ finalw_out, Lay lay_arg, unsigned long long* __restrict__ dbg) {
   const hyg_tg_consts* __restrict__ c = md.consts;
-  const int K = c->K, M = c->M, I = c->I, K2 = 2 * K, tid = threadIdx.x;
+  const int K = KC ? KC : c->K, M = KC ? MC : c->M, I = KC ? 2 * KC + KC * KC : c->I, K2 = 2 * K,
+            tid = threadIdx.x;
+  const Lay lay = KC ? make_layout(KC, MC, BC, MC * (2 * KC + KC * KC), NT, false) : lay_arg;
   // in a register for the whole chain: a load of c-> inside the step loop is a
   // global load the compiler cannot hoist past the record stores (it may
   // alias them), followed by a vmcnt(0) wait on every outstanding store
@@ -1628,16 +1634,18 @@ __device__ __forceinline__ void backward_bits(uint64_t* rb, int B, int t, uint64
   }
 }
 
-template <int NT>
+template <int NT, int KC = 0, int MC = 0, int BC = 0>  // KC > 0: one model shape (see tg_forward_kernel)
 __global__ void __launch_bounds__(NT)
 tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                    const uint8_t* __restrict__ ws, const int32_t* status_in, int16_t* __restrict__ o_merged,
                    int16_t* __restrict__ o_control, int16_t* __restrict__ o_case, float* __restrict__ o_split,
-                   float* __restrict__ o_regime, int32_t* status_out, Lay lay,
+                   float* __restrict__ o_regime, int32_t* status_out, Lay lay_arg,
                    unsigned long long* __restrict__ dbg) {
   const hyg_tg_consts* __restrict__ c = md.consts;
-  const int K = c->K, M = c->M, B = c->B, I = c->I, K2 = 2 * K, tid = threadIdx.x;
-  const int Nmax = c->Nmax;  // hoisted: see sig_thresh in tg_forward_kernel
+  const int K = KC ? KC : c->K, M = KC ? MC : c->M, B = KC ? BC : c->B, I = KC ? 2 * KC + KC * KC : c->I,
+            K2 = 2 * K, tid = threadIdx.x;
+  const int Nmax = KC ? MC * (2 * KC + KC * KC) : c->Nmax;  // hoisted: see sig_thresh in tg_forward_kernel
+  const Lay lay = KC ? make_layout(KC, MC, BC, MC * (2 * KC + KC * KC), NT, true) : lay_arg;
   const ChainDev ch = chains[blockIdx.x];
   const int T = ch.T;
   if (status_in[blockIdx.x] != HYG_OK) return;  // uniform
@@ -2123,6 +2131,28 @@ int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* 
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }
 
+// The kernel instantiation for a launch: the pipeline's model shape (K = 6,
+// M = 50, B = 25, the C3/C4 configurations) at 256 threads has its own
+// compile-time-shaped instantiation (HYG_NO_SHAPE=1: the generic one).
+using FwdFn = decltype(&tg_forward_kernel<64>);
+using BwdFn = decltype(&tg_backward_kernel<64>);
+static bool shape_specialised(const hyg_tg_consts& c) {
+  static const bool off = getenv("HYG_NO_SHAPE") != nullptr;
+  return !off && c.K == 6 && c.M == 50 && c.B == 25 && c.I == 48 && c.Nmax == 2400;
+}
+template <int NT>
+FwdFn fwd_kernel(const hyg_tg_consts& c) {
+  if constexpr (NT == 256)
+    if (shape_specialised(c)) return &tg_forward_kernel<256, 6, 50, 25>;
+  return &tg_forward_kernel<NT>;
+}
+template <int NT>
+BwdFn bwd_kernel(const hyg_tg_consts& c) {
+  if constexpr (NT == 256)
+    if (shape_specialised(c)) return &tg_backward_kernel<256, 6, 50, 25>;
+  return &tg_backward_kernel<NT>;
+}
+
 template <int NT>
 static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
                             const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
@@ -2131,7 +2161,7 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
   static const char* rv = getenv("HYG_TOPSET_R");  // tuning: 1 (A <= 64 per wave) or 2
   if (rv && (atoi(rv) == 1 || atoi(rv) == 2)) lf.topset_r = atoi(rv);
   if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
-  if (hipFuncSetAttribute((const void*)tg_forward_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if (hipFuncSetAttribute((const void*)fwd_kernel<NT>(c), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lf.total) != hipSuccess)
     return HYG_EDEVICE;
   unsigned long long* dbg = nullptr;
@@ -2139,7 +2169,7 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
   if (want_dbg) (void)hipMalloc((void**)&dbg, sizeof(unsigned long long) * kPh * n_chains);
   if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * kPh * n_chains, s);
   ev_record(1, false, s);
-  hipLaunchKernelGGL(tg_forward_kernel<NT>, dim3(n_chains), dim3(NT), lf.total, s, md, chains_dev, E, ws,
+  hipLaunchKernelGGL(fwd_kernel<NT>(c), dim3(n_chains), dim3(NT), lf.total, s, md, chains_dev, E, ws,
                      out.status, out.log_z, out.final_log_weights, lf, dbg);
   ev_record(1, true, s);
   if (hipGetLastError() != hipSuccess) return HYG_EDEVICE;
@@ -2181,7 +2211,7 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
   const Lay lb = make_layout(c.K, c.M, c.B, c.Nmax, NT, true);
   if (lb.total > 160 * 1024) return HYG_EUNSUPPORTED;
   if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
-  if (hipFuncSetAttribute((const void*)tg_backward_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if (hipFuncSetAttribute((const void*)bwd_kernel<NT>(c), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lb.total) != hipSuccess)
     return HYG_EDEVICE;
   static const bool want_dbg = getenv("HYG_DEBUG_PHASES") != nullptr;
@@ -2189,7 +2219,7 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
   if (want_dbg) (void)hipMalloc((void**)&dbgb, sizeof(unsigned long long) * kPh * n_chains);
   if (dbgb) (void)hipMemsetAsync(dbgb, 0, sizeof(unsigned long long) * kPh * n_chains, s);
   ev_record(2, false, s);
-  hipLaunchKernelGGL(tg_backward_kernel<NT>, dim3(n_chains), dim3(NT), lb.total, s, md, chains_dev, E,
+  hipLaunchKernelGGL(bwd_kernel<NT>(c), dim3(n_chains), dim3(NT), lb.total, s, md, chains_dev, E,
                      (const uint8_t*)ws, (const int32_t*)out.status, out.merged, out.control, out.kase,
                      out.split_probs, out.regime_probs, out.status, lb, dbgb);
   ev_record(2, true, s);

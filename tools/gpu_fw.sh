@@ -12,3 +12,7 @@ HYG_DEBUG_PHASES=1 timeout -k 10 200 python bench.py --sites 6000000 --no-cpu-ba
 grep "phases" $O/phases.log
 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 1 --warmup 1 > $O/c3.log 2>&1 || { tail -5 $O/c3.log; exit 1; }
 grep '^{' $O/c3.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('C3', round(d['value']), {k: round(v) for k, v in d['roofline']['kernel_ms'].items()})"
+if [ "$3" = "ab-shape" ]; then
+HYG_NO_SHAPE=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 1 --warmup 1 > $O/c3_noshape.log 2>&1 || { tail -5 $O/c3_noshape.log; exit 1; }
+grep '^{' $O/c3_noshape.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('C3 generic', round(d['value']), {k: round(v) for k, v in d['roofline']['kernel_ms'].items()})"
+fi
