@@ -494,7 +494,13 @@ __device__ __forceinline__ void gen_weights(const ConstLds& cl, int K, int I, in
         cnt += (w > NINF) ? 1 : 0;
       };
       const int K2 = 2 * K;
-      for (int s = wv; s < K2; s += NW) {  // slot types A-D (s is wave-uniform)
+      // Slot loops with trip counts fixed by K (compile-time in the
+      // shape-specialised kernels, so they unroll and the LDS reads of later
+      // slots issue ahead of earlier slots' arithmetic); s is wave-uniform.
+#pragma unroll
+      for (int k = 0; k < (K2 + NW - 1) / NW; ++k) {  // slot types A-D
+        const int s = wv + k * NW;
+        if (s >= K2) break;
         if (s == 0) {
           put(0, (lmA + lcA) + lkA, Ec_rc + Ek_rk);
         } else if (s < K) {  // control change to r != r_k
@@ -509,11 +515,14 @@ __device__ __forceinline__ void gen_weights(const ConstLds& cl, int K, int I, in
           put(s, (lm1 + lcD) + 0.0, Ec_rc + Et[K + arc]);
         }
       }
-      // two change points (i, j): x = (i == j, 1, i, 1, j)
-      int s = wv;
-      while (s < K2) s += NW;
-      int ii = (s - K2) / K, jj = (s - K2) - ii * K;
-      for (; s < I; s += NW) {
+      // two change points (i, j): x = (i == j, 1, i, 1, j), from the wave's
+      // first slot >= 2K
+      const int s0 = wv + NW * ((K2 - wv + NW - 1) / NW);
+#pragma unroll
+      for (int k = 0; k < (I - K2 + NW - 1) / NW; ++k) {
+        const int s = s0 + k * NW;
+        if (s >= I) break;
+        const int ii = (s - K2) / K, jj = (s - K2) - ii * K;
         const double e = Et[ii] + Et[K + jj];
         const double lc = h.lrc + lPcr[ii];
         double lk;
@@ -521,8 +530,6 @@ __device__ __forceinline__ void gen_weights(const ConstLds& cl, int K, int I, in
         else if (ii == ark && am == 0) lk = q.lU1;
         else lk = (jj != ark) ? (h.lrk + ((ii == ark) ? q.lU1 : q.lU2)) : NINF;
         put(s, (((ii == jj) ? lm1 : lm0) + lc) + lk, e);
-        jj += NW;
-        while (jj >= K) { jj -= K; ++ii; }
       }
     }
     *m_out = m;
