@@ -1001,9 +1001,18 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
   lds_barrier();
   TPH(28);
   if (wave_id() == 0) {
-    // lane a: c(a) and the count P(c(a)) (loop-variable semantics of :12-31)
+    // lane a: c(a) (loop-variable semantics of :12-31); the loop's counts
+    // P(c(a)) = #{p : fl(c(a) + x_p) > 0} are taken only at the iterates it
+    // visits, by a ballot over the sorted keys x_p of positions p < min(nA, M)
+    // (one per lane; M <= 64 on this path): the predicate is monotone in p,
+    // so the count of true lanes is the first false position.
     const int a = lane;
-    int Pa = 0, flag = 0;
+    const int cap = nA < M ? nA : M;
+    float xk;
+    if constexpr (R == 1) xk = key_value(e[0]);  // wave 0 lane p holds sorted position p
+    else xk = key_value(srt[lane < nA ? lane : 0]);
+    const uint64_t capmask = (cap >= 64) ? ~0ull : ((1ull << cap) - 1ull);
+    int flag = 0;
     float ca = 0.0f;
     hyg_u192 rva = hyg_u192_zero();
     if (a < M && a < N) {
@@ -1014,25 +1023,18 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
       const double rvd = hyg_u192_to_f64(rva);
       const float l2 = (rvd == 0.0) ? HYG_NINFF : (float)hyg_log(rvd);
       ca = cl.logMa[a] - l2;
-      if (hyg_isfinitef(ca)) {
-        // first p with the predicate false; only min(P, M) matters to the
-        // loop (P >= M ends it), and no weight below sig_thresh can satisfy
-        // it (c < log M + 103.3 there)
-        const int cap = nA < M ? nA : M;
-        int lo = 0, hi = cap;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if ((float)(ca + key_value(srt[mid])) > 0.0f) lo = mid + 1; else hi = mid;
-        }
-        Pa = lo;
-        if (lo == nA && nA < M && hasB) flag = 1;  // the count may continue below A
-      } else if (ca > 0.0f) {
-        Pa = cnt_fin;
-      }
     }
     int aa = 0, bb = -1, ovf = 0;
     while (aa != bb && aa < N && aa < M) {
-      const int nxt = __builtin_amdgcn_readlane(Pa, aa);
+      const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), aa));
+      int nxt = 0;
+      if (hyg_isfinitef(c)) {  // uniform
+        // (no weight below sig_thresh satisfies the predicate: c < log M + 103.3 there)
+        nxt = (int)__builtin_popcountll(wave_ballot((float)(c + xk) > 0.0f) & capmask);
+        if (nxt == nA && nA < M && hasB) ovf = 1;  // the count may continue below A
+      } else if (c > 0.0f) {
+        nxt = cnt_fin;  // +inf: every finite particle
+      }
       ovf |= __builtin_amdgcn_readlane(flag, aa);
       bb = aa;
       aa = nxt > aa ? nxt : aa;
