@@ -207,13 +207,15 @@ __device__ __forceinline__ int wave_incl_int(int v) {
 }
 
 // Block-wide reductions. `red` is an LDS scratch of at least 32 B per wave;
-// every call starts with a barrier so consecutive calls may reuse it.
-template <int NT>
+// every call starts with a barrier so consecutive calls may reuse it
+// (LEAD = false: the caller guarantees that every read of `red` by an earlier
+// reduction is behind a barrier already, e.g. its own slot of `red`).
+template <int NT, bool LEAD = true>
 __device__ __forceinline__ void block_max_cnt(double m, int c, unsigned char* red, double* m_out, int* c_out) {
   m = wave_max(m);
   c = wave_sum(c);
   if (NT == 64) { *m_out = m; *c_out = c; return; }
-  lds_barrier();
+  if constexpr (LEAD) lds_barrier();
   if (lane_id() == 0) {
     ((double*)red)[2 * wave_id()] = m;
     ((int*)red)[4 * wave_id() + 2] = c;
@@ -239,12 +241,12 @@ __device__ __forceinline__ double block_max(double v, unsigned char* red) {
   for (int w = 1; w < NT / 64; ++w) m = dmax(m, ((double*)red)[w]);
   return m;
 }
-template <int NT>
+template <int NT, bool LEAD = true>
 __device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red) {
   hyg_u128* r = (hyg_u128*)red;
   v = wave_sum128(v);
   if (NT == 64) return v;
-  lds_barrier();
+  if constexpr (LEAD) lds_barrier();
   if (lane_id() == 0) r[wave_id()] = v;
   lds_barrier();
   hyg_u128 s = hyg_u128_zero();
@@ -269,13 +271,13 @@ __device__ __forceinline__ bool block_or(bool p, unsigned char* red) {
 // Exclusive block scans. The register forms return this thread's exclusive
 // prefix and the block total; the array form writes out[tid] (exclusive) and
 // out[NT] (total) for searches.
-template <int NT>
+template <int NT, bool LEAD = true>
 __device__ __forceinline__ hyg_u192 block_excl192(hyg_u192 v, unsigned char* red, hyg_u192* total) {
   hyg_u192* r = (hyg_u192*)red;
   const hyg_u192 inc = wave_incl192(v);
   hyg_u192 wt;  // this wave's total
   wt.w0 = rdlane64(inc.w0, 63); wt.w1 = rdlane64(inc.w1, 63); wt.w2 = rdlane64(inc.w2, 63);
-  lds_barrier();
+  if constexpr (LEAD) lds_barrier();
   if (lane_id() == 0) r[wave_id()] = wt;
   lds_barrier();
   hyg_u192 pre = hyg_u192_zero(), tot = hyg_u192_zero();

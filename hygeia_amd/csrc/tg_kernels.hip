@@ -373,7 +373,7 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
     l.gst = o; o = align_up(o + sizeof(uint64_t) * B, 16);
     l.rb = o; o = align_up(o + 2 * sizeof(uint64_t) * ((B + 3) / 4) * 4, 16);  // draw bits, two steps
   }
-  l.red = o; o = align_up(o + 32 * (NT / 64), 16);
+  l.red = o; o = align_up(o + 2 * 32 * (NT / 64), 16);  // two slots: the step's log-sum-exp has its own
   l.sh = o; o = align_up(o + sizeof(Shared), 16);
   l.total = o;
   return l;
@@ -989,7 +989,9 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
     loc = hyg_u192_add(loc, f[r]);
   }
   hyg_u192 massA;
-  const hyg_u192 ex = block_excl192<NT>(loc, red, &massA);  // its barriers end every sort-buffer read
+  // red's last readers (the previous step's block max) are behind this step's
+  // barriers; its publishing barrier ends every sort-buffer read
+  const hyg_u192 ex = block_excl192<NT, false>(loc, red, &massA);
   hyg_u192* pre = (hyg_u192*)scr;                           // inclusive prefix of sorted position p
   const hyg_u192 total = hyg_u192_add(massA, massB);         // every significant weight's mass
   hyg_u192 run = ex;
@@ -1364,7 +1366,9 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       }
       const hyg_u128 sacc = hyg_u128_add(s0, s1);
       PH(12);
-      const hyg_u128 S = block_sum128<NT>(sacc, red);
+      // own slot of `red`, whose last reader (this reduction, a step ago) is
+      // behind many barriers: no leading barrier
+      const hyg_u128 S = block_sum128<NT, false>(sacc, red + 32 * (NT / 64));
       PH(11);
       logS = hyg_log(hyg_u128_to_f64(S, 100));
     }
@@ -1552,7 +1556,8 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       }
     }
     PH(8);
-    block_max_cnt<NT>(mloc, cloc, red, &mx, &cnt);
+    // (every read of red by this step's resampling is behind the gather's barriers)
+    block_max_cnt<NT, false>(mloc, cloc, red, &mx, &cnt);
     PH(6);
   }
   // ---- final weights: log normalising constant and run()'s second output
