@@ -32,6 +32,20 @@ namespace hyg {
 
 enum { MODE_KEEP = 0, MODE_OPTIMAL = 1, MODE_UNBIASED = 2, MODE_INIT = 3 };
 
+// Wave priority of the single-wave serial sections (the K loop + systematic
+// draws, the backward's one-wave categorical): while one wave of a chain works
+// alone, the others wait at a barrier, so its issue slots are the chain's
+// critical path; the other chains sharing the CU fill the gaps.
+#ifndef HYG_SERIAL_PRIO
+#define HYG_SERIAL_PRIO 1
+#endif
+__device__ __forceinline__ void serial_begin() {
+  if constexpr (HYG_SERIAL_PRIO > 0) __builtin_amdgcn_s_setprio(HYG_SERIAL_PRIO);
+}
+__device__ __forceinline__ void serial_end() {
+  if constexpr (HYG_SERIAL_PRIO > 0) __builtin_amdgcn_s_setprio(0);
+}
+
 
 // sort key: ascending key == descending f32 value, ties by ascending index
 __device__ __forceinline__ uint64_t sort_key(float x, int idx) {
@@ -1003,6 +1017,7 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
   lds_barrier();
   TPH(28);
   if (wave_id() == 0) {
+    serial_begin();
     // lane a: c(a) (loop-variable semantics of :12-31); the loop's counts
     // P(c(a)) = #{p : fl(c(a) + x_p) > 0} are taken only at the iterates it
     // visits, by a ballot over the sorted keys x_p of positions p < min(nA, M)
@@ -1073,6 +1088,7 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
       sh.log_c = lc;
       sh.fast = status;
     }
+    serial_end();
   }
   lds_barrier();
   TPH(29);
@@ -1826,6 +1842,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       // ---- backward-kernel rows (:400-435), one per distinct next state
       if (B <= 64) {
         if (wave_id() == 0) {
+          serial_begin();
           const int lane = lane_id();
           int g = -1;
           if (lane < B) {
@@ -1841,6 +1858,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             if (g == lane) gst[gi] = X[lane];
           }
           if (lane == 0) sh.ng = __popcll(lead);
+          serial_end();
         }
       } else if (tid == 0) {
         int ng = 0;
@@ -1939,6 +1957,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         if (L <= 64 && B <= 64 && Nmax >= 192) {
           // ---- one wave: order the list by n, exact masses, scan, draws
           if (wave_id() == 0) {
+            serial_begin();
             const int lane = lane_id();
             const bool v = lane < L;
             const int myn = v ? lst_n[lane] : 0x7fffffff;
@@ -1971,6 +1990,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
               }
               idx[lane] = lst_n[lo];
             }
+            serial_end();
           }
           BPH(4);
         } else {
@@ -2015,6 +2035,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
     }
     if (B <= 64 && wave_id() == 0) {  // trajectory b on lane b of wave 0 (its own X write): means by ballots
+      serial_begin();
       const int lane = lane_id();
       const bool v = lane < B;
       const uint64_t x = v ? X[lane] : 0ull;
@@ -2029,6 +2050,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         if (lane == 0) o_split[ch.out_begin + t] = vv;
         else o_regime[(size_t)(ch.out_begin + t) * K2 + (lane - 1)] = vv;
       }
+      serial_end();
     }
     BPH(6);
     // ---- record t-1 (+ hazard rows) replaces record t once every read of it is done

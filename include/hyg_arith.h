@@ -208,10 +208,37 @@ HYG_HD int hyg_clz64(uint64_t x) { return x ? __builtin_clzll(x) : 64; }
 typedef struct { uint64_t lo, hi; } hyg_u128;
 
 HYG_HD hyg_u128 hyg_u128_zero(void) { hyg_u128 r; r.lo = 0; r.hi = 0; return r; }
+#if defined(__HIPCC__)
+/* Multiword add / subtract / compare as 32-bit carry chains (v_add_co_u32 +
+ * v_addc_co_u32 on the GPU: 4 VALU ops per u128 add, 6 per u192, instead of
+ * 64-bit adds with compare-and-select carries). Same integers as the C forms
+ * below, which the gcc-built oracle uses. */
+#define HYG__L32(x) ((unsigned)(x))
+#define HYG__H32(x) ((unsigned)((x) >> 32))
+#define HYG__J64(l, h) ((uint64_t)(l) | ((uint64_t)(h) << 32))
+HYG_HD hyg_u128 hyg_u128_add(hyg_u128 a, hyg_u128 b) {
+  unsigned c0, c1, c2, c3;
+  const unsigned r0 = __builtin_addc(HYG__L32(a.lo), HYG__L32(b.lo), 0u, &c0);
+  const unsigned r1 = __builtin_addc(HYG__H32(a.lo), HYG__H32(b.lo), c0, &c1);
+  const unsigned r2 = __builtin_addc(HYG__L32(a.hi), HYG__L32(b.hi), c1, &c2);
+  const unsigned r3 = __builtin_addc(HYG__H32(a.hi), HYG__H32(b.hi), c2, &c3);
+  hyg_u128 r; r.lo = HYG__J64(r0, r1); r.hi = HYG__J64(r2, r3); return r;
+}
+/* a < b: the borrow out of a - b */
+HYG_HD int hyg_u128_lt(hyg_u128 a, hyg_u128 b) {
+  unsigned c0, c1, c2, c3;
+  (void)__builtin_subc(HYG__L32(a.lo), HYG__L32(b.lo), 0u, &c0);
+  (void)__builtin_subc(HYG__H32(a.lo), HYG__H32(b.lo), c0, &c1);
+  (void)__builtin_subc(HYG__L32(a.hi), HYG__L32(b.hi), c1, &c2);
+  (void)__builtin_subc(HYG__H32(a.hi), HYG__H32(b.hi), c2, &c3);
+  return (int)c3;
+}
+#else
 HYG_HD hyg_u128 hyg_u128_add(hyg_u128 a, hyg_u128 b) {
   hyg_u128 r; r.lo = a.lo + b.lo; r.hi = a.hi + b.hi + (r.lo < a.lo ? 1u : 0u); return r;
 }
 HYG_HD int hyg_u128_lt(hyg_u128 a, hyg_u128 b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
+#endif
 HYG_HD int hyg_u128_is_zero(hyg_u128 a) { return (a.lo | a.hi) == 0; }
 
 /* floor(e * 2^100) for e in [0, 2^16) (masses are in [0, 1]); masses below
@@ -257,6 +284,39 @@ HYG_HD double hyg_u128_to_f64(hyg_u128 a, int scale) {
 typedef struct { uint64_t w0, w1, w2; } hyg_u192;
 
 HYG_HD hyg_u192 hyg_u192_zero(void) { hyg_u192 r; r.w0 = 0; r.w1 = 0; r.w2 = 0; return r; }
+#if defined(__HIPCC__)
+HYG_HD hyg_u192 hyg_u192_add(hyg_u192 a, hyg_u192 b) {
+  unsigned c0, c1, c2, c3, c4, c5;
+  const unsigned r0 = __builtin_addc(HYG__L32(a.w0), HYG__L32(b.w0), 0u, &c0);
+  const unsigned r1 = __builtin_addc(HYG__H32(a.w0), HYG__H32(b.w0), c0, &c1);
+  const unsigned r2 = __builtin_addc(HYG__L32(a.w1), HYG__L32(b.w1), c1, &c2);
+  const unsigned r3 = __builtin_addc(HYG__H32(a.w1), HYG__H32(b.w1), c2, &c3);
+  const unsigned r4 = __builtin_addc(HYG__L32(a.w2), HYG__L32(b.w2), c3, &c4);
+  const unsigned r5 = __builtin_addc(HYG__H32(a.w2), HYG__H32(b.w2), c4, &c5);
+  hyg_u192 r; r.w0 = HYG__J64(r0, r1); r.w1 = HYG__J64(r2, r3); r.w2 = HYG__J64(r4, r5); return r;
+}
+HYG_HD hyg_u192 hyg_u192_sub(hyg_u192 a, hyg_u192 b) { /* a >= b */
+  unsigned c0, c1, c2, c3, c4, c5;
+  const unsigned r0 = __builtin_subc(HYG__L32(a.w0), HYG__L32(b.w0), 0u, &c0);
+  const unsigned r1 = __builtin_subc(HYG__H32(a.w0), HYG__H32(b.w0), c0, &c1);
+  const unsigned r2 = __builtin_subc(HYG__L32(a.w1), HYG__L32(b.w1), c1, &c2);
+  const unsigned r3 = __builtin_subc(HYG__H32(a.w1), HYG__H32(b.w1), c2, &c3);
+  const unsigned r4 = __builtin_subc(HYG__L32(a.w2), HYG__L32(b.w2), c3, &c4);
+  const unsigned r5 = __builtin_subc(HYG__H32(a.w2), HYG__H32(b.w2), c4, &c5);
+  hyg_u192 r; r.w0 = HYG__J64(r0, r1); r.w1 = HYG__J64(r2, r3); r.w2 = HYG__J64(r4, r5); return r;
+}
+/* a >= b: no borrow out of a - b */
+HYG_HD int hyg_u192_ge(hyg_u192 a, hyg_u192 b) {
+  unsigned c0, c1, c2, c3, c4, c5;
+  (void)__builtin_subc(HYG__L32(a.w0), HYG__L32(b.w0), 0u, &c0);
+  (void)__builtin_subc(HYG__H32(a.w0), HYG__H32(b.w0), c0, &c1);
+  (void)__builtin_subc(HYG__L32(a.w1), HYG__L32(b.w1), c1, &c2);
+  (void)__builtin_subc(HYG__H32(a.w1), HYG__H32(b.w1), c2, &c3);
+  (void)__builtin_subc(HYG__L32(a.w2), HYG__L32(b.w2), c3, &c4);
+  (void)__builtin_subc(HYG__H32(a.w2), HYG__H32(b.w2), c4, &c5);
+  return (int)(c5 ^ 1u);
+}
+#else
 HYG_HD hyg_u192 hyg_u192_add(hyg_u192 a, hyg_u192 b) {
   hyg_u192 r;
   r.w0 = a.w0 + b.w0;
@@ -279,6 +339,12 @@ HYG_HD hyg_u192 hyg_u192_sub(hyg_u192 a, hyg_u192 b) { /* a >= b */
   r.w2 = a.w2 - b.w2 - br1a - br1b;
   return r;
 }
+HYG_HD int hyg_u192_ge(hyg_u192 a, hyg_u192 b) {
+  if (a.w2 != b.w2) return a.w2 > b.w2;
+  if (a.w1 != b.w1) return a.w1 > b.w1;
+  return a.w0 >= b.w0;
+}
+#endif
 HYG_HD int hyg_u192_is_zero(hyg_u192 a) { return (a.w0 | a.w1 | a.w2) == 0; }
 
 /* exact integer image of an f32 mass m in [0, 1]: m * 2^149. */
@@ -328,12 +394,6 @@ HYG_HD double hyg_u192_to_f64(hyg_u192 a) {
   }
   top &= 0x001fffffffffffffull;
   return (double)top * hyg_pow2(sh - 149);
-}
-
-HYG_HD int hyg_u192_ge(hyg_u192 a, hyg_u192 b) {
-  if (a.w2 != b.w2) return a.w2 > b.w2;
-  if (a.w1 != b.w1) return a.w1 > b.w1;
-  return a.w0 >= b.w0;
 }
 
 /* ceil(T * R) for an f32 T in [0, 1] and R < 2^151 (R = value * 2^149 as
