@@ -1220,11 +1220,14 @@ tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
 // M = 50, B = 25): K, M, B, the candidate count and the whole LDS layout are
 // then compile-time constants (LDS addresses fold into instruction offsets,
 // loops over slots get constant trip counts); KC = 0 reads them at run time.
-template <int NT, int KC = 0, int MC = 0, int BC = 0>
+template <int NT, int KC = 0, int MC = 0, int BC = 0, bool PHS = false>  // PHS: phase-timer build
 __global__ void __launch_bounds__(NT, (NT <= 256 ? 3 : 1))
 tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                   uint8_t* __restrict__ ws, int32_t* status_out, double* __restrict__ logz_out,
-                  double* __restrict__ finalw_out, Lay lay_arg, unsigned long long* __restrict__ dbg) {
+                  double* __restrict__ finalw_out, Lay lay_arg, unsigned long long* __restrict__ dbg_arg) {
+  // the timers only exist in the PHS instantiation: a constant null pointer
+  // folds every timer test away (no SGPRs, branches or s_memtime in the step loop)
+  unsigned long long* __restrict__ const dbg = PHS ? dbg_arg : nullptr;
   const hyg_tg_consts* __restrict__ c = md.consts;
   const int K = KC ? KC : c->K, M = KC ? MC : c->M, I = KC ? 2 * KC + KC * KC : c->I, K2 = 2 * K,
             tid = threadIdx.x;
@@ -1664,13 +1667,14 @@ __device__ __forceinline__ void backward_bits(uint64_t* rb, int B, int t, uint64
   }
 }
 
-template <int NT, int KC = 0, int MC = 0, int BC = 0>  // KC > 0: one model shape (see tg_forward_kernel)
+template <int NT, int KC = 0, int MC = 0, int BC = 0, bool PHS = false>  // KC > 0: one model shape (see tg_forward_kernel)
 __global__ void __launch_bounds__(NT)
 tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                    const uint8_t* __restrict__ ws, const int32_t* status_in, int16_t* __restrict__ o_merged,
                    int16_t* __restrict__ o_control, int16_t* __restrict__ o_case, float* __restrict__ o_split,
                    float* __restrict__ o_regime, int32_t* status_out, Lay lay_arg,
-                   unsigned long long* __restrict__ dbg) {
+                   unsigned long long* __restrict__ dbg_arg) {
+  unsigned long long* __restrict__ const dbg = PHS ? dbg_arg : nullptr;  // (see tg_forward_kernel)
   const hyg_tg_consts* __restrict__ c = md.consts;
   const int K = KC ? KC : c->K, M = KC ? MC : c->M, B = KC ? BC : c->B, I = KC ? 2 * KC + KC * KC : c->I,
             K2 = 2 * K, tid = threadIdx.x;
@@ -2176,14 +2180,35 @@ static bool shape_specialised(const hyg_tg_consts& c) {
   static const bool off = getenv("HYG_NO_SHAPE") != nullptr;
   return !off && c.K == 6 && c.M == 50 && c.B == 25 && c.I == 48 && c.Nmax == 2400;
 }
+// HYG_DEBUG_PHASES=1 selects the phase-timer instantiations (256 and 512 threads).
+static bool want_phases() {
+  static const bool on = getenv("HYG_DEBUG_PHASES") != nullptr;
+  return on;
+}
+template <int NT>
+constexpr bool has_phases() { return NT == 256 || NT == 512; }
 template <int NT>
 FwdFn fwd_kernel(const hyg_tg_consts& c) {
+  if constexpr (has_phases<NT>()) {
+    if (want_phases()) {
+      if constexpr (NT == 256)
+        if (shape_specialised(c)) return &tg_forward_kernel<256, 6, 50, 25, true>;
+      return &tg_forward_kernel<NT, 0, 0, 0, true>;
+    }
+  }
   if constexpr (NT == 256)
     if (shape_specialised(c)) return &tg_forward_kernel<256, 6, 50, 25>;
   return &tg_forward_kernel<NT>;
 }
 template <int NT>
 BwdFn bwd_kernel(const hyg_tg_consts& c) {
+  if constexpr (has_phases<NT>()) {
+    if (want_phases()) {
+      if constexpr (NT == 256)
+        if (shape_specialised(c)) return &tg_backward_kernel<256, 6, 50, 25, true>;
+      return &tg_backward_kernel<NT, 0, 0, 0, true>;
+    }
+  }
   if constexpr (NT == 256)
     if (shape_specialised(c)) return &tg_backward_kernel<256, 6, 50, 25>;
   return &tg_backward_kernel<NT>;
@@ -2201,7 +2226,7 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
                           (int)lf.total) != hipSuccess)
     return HYG_EDEVICE;
   unsigned long long* dbg = nullptr;
-  static const bool want_dbg = getenv("HYG_DEBUG_PHASES") != nullptr;
+  const bool want_dbg = has_phases<NT>() && want_phases();
   if (want_dbg) (void)hipMalloc((void**)&dbg, sizeof(unsigned long long) * kPh * n_chains);
   if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * kPh * n_chains, s);
   ev_record(1, false, s);
@@ -2250,7 +2275,7 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
   if (hipFuncSetAttribute((const void*)bwd_kernel<NT>(c), hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lb.total) != hipSuccess)
     return HYG_EDEVICE;
-  static const bool want_dbg = getenv("HYG_DEBUG_PHASES") != nullptr;
+  const bool want_dbg = has_phases<NT>() && want_phases();
   unsigned long long* dbgb = nullptr;
   if (want_dbg) (void)hipMalloc((void**)&dbgb, sizeof(unsigned long long) * kPh * n_chains);
   if (dbgb) (void)hipMemsetAsync(dbgb, 0, sizeof(unsigned long long) * kPh * n_chains, s);
