@@ -412,11 +412,13 @@ __device__ __forceinline__ void sg_smoother(const SgModelDev md, const SgChainDe
                                             uint8_t* __restrict__ ws, int cap, double* __restrict__ probs,
                                             int32_t* __restrict__ status_out, const SgCLay lay);
 
-template <int KT, int NB, bool PE>
+template <int KT, int NB, bool PE, bool PHS = false>  // PHS: the phase-timer build (HYG_SG_PHASES)
 __global__ void __launch_bounds__(NB)
 sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chains, const double* __restrict__ E,
                 uint8_t* __restrict__ ws, int cap, double* __restrict__ probs, int32_t* __restrict__ status_out,
-                SgLay lay, SgCLay clay, unsigned long long* __restrict__ dbg, SgPeDev pe) {
+                SgLay lay, SgCLay clay, unsigned long long* __restrict__ dbg_arg, SgPeDev pe) {
+  // a constant null pointer outside the timer build: every timer test folds away
+  unsigned long long* __restrict__ const dbg = PHS ? dbg_arg : nullptr;
   // blocks [0, n_chains): the SMC of chain b; blocks [n_chains, 2 n_chains):
   // the online marginal smoothing of chain b - n_chains, fed by the ring
   if ((int)blockIdx.x >= n_chains) {
@@ -1361,13 +1363,13 @@ __device__ __forceinline__ void sg_smoother(const SgModelDev md, const SgChainDe
 // One launch per group of at most (CUs / 2) chains: the SMC and the smoothing
 // workgroup of every chain must be co-resident (one workgroup per CU at this
 // LDS size), since each waits for the other through the ring.
-template <int KT, int NB, bool PE>
+template <int KT, int NB, bool PE, bool PHS = false>
 static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, int n_chains, const double* E,
                             uint8_t* ws, int cap, double* probs, int32_t* status, const SgLay& lay,
                             const SgCLay& clay, size_t lds, unsigned long long* dbg, hipStream_t s, const SgPeDev& pe,
                             hipError_t* err) {
-  *err = hipFuncSetAttribute((const void*)sg_chain_kernel<KT, NB, PE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds);
+  *err = hipFuncSetAttribute((const void*)sg_chain_kernel<KT, NB, PE, PHS>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (*err != hipSuccess) return;
   int dev = 0, cus = 0;
   if ((*err = hipGetDevice(&dev)) != hipSuccess) return;
@@ -1375,7 +1377,7 @@ static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, 
   const int per = cus / 2 > 0 ? cus / 2 : 1;
   for (int c0 = 0; c0 < n_chains; c0 += per) {
     const int nc = (n_chains - c0) < per ? (n_chains - c0) : per;
-    hipLaunchKernelGGL((sg_chain_kernel<KT, NB, PE>), dim3(2 * nc), dim3(NB), lds, s, md, chains_dev + c0, nc, E,
+    hipLaunchKernelGGL((sg_chain_kernel<KT, NB, PE, PHS>), dim3(2 * nc), dim3(NB), lds, s, md, chains_dev + c0, nc, E,
                        ws, cap, probs, status + c0, lay, clay, dbg ? dbg + (size_t)16 * c0 : nullptr, pe);
     if ((*err = hipGetLastError()) != hipSuccess) return;
   }
@@ -1403,7 +1405,9 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
   SgPeDev ped{};
   if (pe) ped = *pe;
   if (lds > kSgLdsBudget) return HYG_EUNSUPPORTED;
-  static const bool want_dbg = getenv("HYG_SG_PHASES") != nullptr;
+  // phase timers: HYG_SG_PHASES=1, in the K = 6 instantiations (the pipeline's shape) only
+  static const bool want_env = getenv("HYG_SG_PHASES") != nullptr;
+  const bool want_dbg = want_env && c.K == 6;
   unsigned long long* dbg = nullptr;
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(ctl, 0, kSgCtlBytes * (size_t)n_chains, s) != hipSuccess) return HYG_EDEVICE;
@@ -1413,7 +1417,14 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
   switch (c.K) {
 #define SG_CASE(k)                                                                                               \
   case k:                                                                                                        \
-    if (pe)                                                                                                      \
+    if (k == 6 && dbg) {                                                                                         \
+      if (pe)                                                                                                    \
+        launch_chain_kt<6, 512, true, true>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, clay,   \
+                                            lds, dbg, s, ped, &err);                                             \
+      else                                                                                                       \
+        launch_chain_kt<6, 512, false, true>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, clay,  \
+                                             lds, dbg, s, ped, &err);                                            \
+    } else if (pe)                                                                                               \
       launch_chain_kt<k, (k <= 8 ? 512 : 256), true>(md, chains_dev, n_chains, E, ws, psi_cap, probs, status, lay, \
                                                      clay, lds, dbg, s, ped, &err);                              \
     else                                                                                                         \

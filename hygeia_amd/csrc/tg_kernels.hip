@@ -1316,7 +1316,8 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       // kCC candidates per lane at a time, their loads issued together (a
       // load / compare / ballot per iteration waits out an LDS round trip each)
       const double cutw = (double)sig_thresh;
-      constexpr int kCC = 8;
+      // (the shape-specialised kernel: every candidate in one pass, N <= M I)
+      constexpr int kCC = KC ? (MC * (2 * KC + KC * KC) + NT - 1) / NT : 8;
       for (int b0 = wave_id() * 64; b0 < N; b0 += kCC * NT) {
         bool keep[kCC];
 #pragma unroll
