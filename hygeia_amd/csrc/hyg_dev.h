@@ -64,17 +64,44 @@ __device__ __forceinline__ uint32_t xshfl32(uint32_t v) {
   } else if constexpr (LM == 2) {
     return dpp32<kDppQuad2301>(v);
   } else if constexpr (LM == 4) {
-    const uint32_t up = dpp32<0x104>(v), dn = dpp32<0x114>(v);  // row_shl:4 / row_shr:4
-    return (threadIdx.x & 4) ? dn : up;
+    // row_shl:4 everywhere, then row_shr:4 merged into banks 1 and 3 (lanes
+    // with bit 2 set) by the DPP bank mask: no lane-mask select
+    const uint32_t up = dpp32<0x104>(v);
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)up, (int)v, 0x114, 0xf, 0xa, false);
   } else if constexpr (LM == 8) {
     return dpp32<0x128>(v);  // row_ror:8
   } else if constexpr (LM == 16) {
+    // lanes with bit 4 set take r[0], the others r[1]: r[1] merged into rows
+    // 0 and 2 by an identity DPP move with a row mask (a lane-mask select would
+    // be a loop-invariant SGPR pair the compiler spills and reloads per use)
     const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (threadIdx.x & 16) ? r[0] : r[1];
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)r[0], (int)r[1], 0xE4, 0x5, 0xf, false);
   } else {
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return (threadIdx.x & 32) ? r[0] : r[1];
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // rows 0-1 take r[1]
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)r[0], (int)r[1], 0xE4, 0x3, 0xf, false);
   }
+}
+// Lanes l of a wave with (l & j) == 0, for j = 1, 2, ..., 32 (a constant after unrolling)
+__device__ __forceinline__ constexpr uint64_t lanes_bit_clear(int j) {
+  return j == 1 ? 0x5555555555555555ull
+       : j == 2 ? 0x3333333333333333ull
+       : j == 4 ? 0x0F0F0F0F0F0F0F0Full
+       : j == 8 ? 0x00FF00FF00FF00FFull
+       : j == 16 ? 0x0000FFFF0000FFFFull
+                 : 0x00000000FFFFFFFFull;
+}
+// Per-lane select by a wave-uniform lane mask: bit l set -> if1 on lane l.
+// v_cndmask with the mask in an SGPR pair, written directly: built from a
+// constant lane pattern by scalar ops, the mask stays rematerialisable.
+__device__ __forceinline__ uint32_t lane_select32(uint64_t m, uint32_t if0, uint32_t if1) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
+  return r;
+}
+__device__ __forceinline__ uint64_t lane_select64(uint64_t m, uint64_t if0, uint64_t if1) {
+  const uint32_t lo = lane_select32(m, (uint32_t)if0, (uint32_t)if1);
+  const uint32_t hi = lane_select32(m, (uint32_t)(if0 >> 32), (uint32_t)(if1 >> 32));
+  return ((uint64_t)hi << 32) | lo;
 }
 template <int LM>
 __device__ __forceinline__ uint64_t xshfl64(uint64_t v) {

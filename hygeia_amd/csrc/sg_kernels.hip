@@ -389,7 +389,19 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
           default: pk = xshfl64<32>(key); pi = (int)xshfl32<32>((uint32_t)idx); break;
         }
       }
-      if (real) {
+      if (j < 64) {
+        if (real) {
+          // (lower == up) is a constant lane pattern (k >= 64: a wave bit), so
+          // the exchange is the compare's lane mask xnor that pattern
+          const uint64_t lower = lanes_bit_clear(j);
+          const uint64_t same = (k < 64) ? ~(lower ^ lanes_bit_clear(k < 64 ? k : 1))
+                                         : (((wave_id() * 64) & k) == 0 ? lower : ~lower);
+          const uint64_t pf = wave_ballot(pk > key || (pk == key && pi < idx));
+          const uint64_t take = ~(same ^ pf);
+          key = lane_select64(take, key, pk);
+          idx = (int)lane_select32(take, (uint32_t)idx, (uint32_t)pi);
+        }
+      } else if (real) {
         const bool up = (tid & k) == 0, lower = (tid & j) == 0;
         const bool pfirst = pk > key || (pk == key && pi < idx);
         if ((lower == up) ? pfirst : !pfirst) {

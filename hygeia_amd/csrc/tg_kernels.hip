@@ -924,6 +924,19 @@ __device__ __forceinline__ double cut_below_top(int k) {
                : (k < 6 ? (k == 4 ? 26.0 : 30.0) : 36.0);
 }
 
+// Lanes l of a wave whose key keeps the minimum at stage (KK, J) of the
+// bitonic sort below, for J in [R, 64R) and the wave bit of i clear
+template <int R, int J, int KK>
+constexpr uint64_t keep_min_pattern() {
+  uint64_t m = 0;
+  for (int l = 0; l < 64; ++l) {
+    const bool a = (l & (J / R)) == 0;
+    const bool b = (KK < 64 * R) ? ((l & (KK / R)) == 0) : true;
+    if (a == b) m |= 1ull << l;
+  }
+  return m;
+}
+
 // One compare-exchange stage (k, j) of a bitonic sort of 64*NW*R keys held
 // R per lane, key index i = wave*64R + lane*R + r (ascending result).
 // j < R: inside the lane; j < 64R: lane xor shuffles; else: LDS + barrier.
@@ -944,13 +957,17 @@ __device__ __forceinline__ void bitonic_stage(uint64_t (&e)[R], uint64_t* buf, i
       }
     }
   } else if constexpr (J < 64 * R) {
+    // keep_min = ((i & J) == 0) == ((i & KK) == 0) for i = wave 64R + lane R + r
+    // is a constant lane pattern (J, and KK < 64R, select lane bits; KK >= 64R a
+    // wave bit): the exchange is the compare's lane mask xnor that pattern
+    constexpr uint64_t pat = keep_min_pattern<R, J, KK>();
+    const bool wflip = (KK >= 64 * R) && (((wave_id() * 64 * R) & KK) != 0);  // wave-uniform
+    const uint64_t keep = wflip ? ~pat : pat;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const uint64_t o = xshfl64<J / R>(e[r]);
-      const int i = base + r;
-      const bool keep_min = ((i & J) == 0) == ((i & KK) == 0);
-      const bool lt = o < e[r];
-      e[r] = (keep_min == lt) ? o : e[r];
+      const uint64_t lt = wave_ballot(o < e[r]);
+      e[r] = lane_select64(~(keep ^ lt), e[r], o);
     }
   } else {
     uint64_t* b = buf + (ib & 1) * n;  // alternate buffers: one barrier per stage
