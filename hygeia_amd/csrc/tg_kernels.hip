@@ -323,6 +323,7 @@ struct Shared {  // broadcast scalars of one workgroup
   float Unext;  // systematic-resampling uniform of the next step, drawn during the gather
   unsigned sig_ctr;
   hyg_u192 R, preK;
+  int segc[16];  // backward: finite logits per reachable slot (segment list)
   unsigned long long ph[kPh];
 };
 
@@ -1903,8 +1904,23 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
                   rkn = hyg_st_rk(xn);
         // ---- finite logits l_n = log f(xn | x_n) + W_n, gathered into a short
         //      list (n, l_n): only a few dozen of the N candidates can reach xn
-        if (tid == 0) sh.cnt = 0;
-        lds_barrier();
+        // Only slots whose child can have d_c = dcn - 1 (or a control change
+        // point when dcn = 1) can reach xn: lc of tg_trans is a constant -inf
+        // otherwise (ancestors always have d_c >= 1).
+        int r0a, r0b, r1a, r1b;
+        if (dcn >= 3) { r0a = 0; r0b = 1; r1a = K; r1b = 2 * K; }                         // A, C, D
+        else if (dcn == 2) { r0a = 1; r0b = K; r1a = 2 * K + rcn * K; r1b = r1a + K; }   // B, E(i = rcn)
+        else { r0a = 0; r0b = I; r1a = I; r1b = I; }
+        const int nseg0 = r0b - r0a, nseg = nseg0 + (r1b - r1a);
+        // Segment list (at most kSeg reachable slots): slot v's finite logits
+        // at [64 v, 64 v + c_v) in lane order, so the list is in n order by
+        // construction: no shared counter, no atomics, no rank sort
+        constexpr int kSeg = 16;
+        const bool segp = fast && nseg <= kSeg && Nmax >= 64 * kSeg + 160 && 4 * (NT + 1) >= 64 * kSeg;
+        if (!segp) {
+          if (tid == 0) sh.cnt = 0;
+          lds_barrier();  // (the segment path: every reader of the areas is behind the last group's barrier)
+        }
         int* lst_n = (int*)cp128;  // list indices (cp area, NT+1 u128 = 4(NT+1) ints)
         double* lst_l = Lg;        // list logits
         const int cap = (4 * (NT + 1) < Nmax) ? 4 * (NT + 1) : Nmax;
@@ -1930,19 +1946,16 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
                     ark = hyg_st_rk(par);
           Pf3 pa{};
           if (act) pa = PF[lane];
-          // Only slots whose child can have d_c = dcn - 1 (or a control change
-          // point when dcn = 1) can reach xn: lc of tg_trans is a constant -inf
-          // otherwise (ancestors always have d_c >= 1).
-          int r0a, r0b, r1a, r1b;
-          if (dcn >= 3) { r0a = 0; r0b = 1; r1a = K; r1b = 2 * K; }                         // A, C, D
-          else if (dcn == 2) { r0a = 1; r0b = K; r1a = 2 * K + rcn * K; r1b = r1a + K; }   // B, E(i = rcn)
-          else { r0a = 0; r0b = I; r1a = I; r1b = I; }
           for (int part = 0; part < 2; ++part) {
             const int sa = part ? r1a : r0a, sb = part ? r1b : r0b;
             for (int sl = sa + wv; sl < sb; sl += NW) {
+              const int sgv = part ? nseg0 + (sl - r1a) : (sl - r0a);  // segment of slot sl
               const Child x = child_of(cl, K, am, adc, arc, adk, ark, pa, sl);
               const bool poss = act && trans_possible(cl.u, x, mn, dcn, rcn, dkn, rkn);
-              if (__ballot(poss) == 0) continue;  // nothing in this slot reaches xn
+              if (__ballot(poss) == 0) {  // nothing in this slot reaches xn
+                if (segp && lane == 0) sh.segc[sgv] = 0;
+                continue;
+              }
               double l = HYG_NINF;
               if (poss) {
                 const double w = weight_at(cl, K, lane, sl, s.mode, s.log_c, s.lse, P, pw, PHZ, Et);
@@ -1953,7 +1966,14 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
                 }
               }
               const unsigned long long mask = __ballot(l > HYG_NINF);
-              if (mask) {
+              if (segp) {
+                if (lane == 0) sh.segc[sgv] = (int)__popcll(mask);
+                if (l > HYG_NINF) {
+                  const int pos = 64 * sgv + lanes_below(mask);
+                  lst_n[pos] = sl * np + lane;
+                  lst_l[pos] = l;
+                }
+              } else if (mask) {
                 int base = 0;
                 if (lane == 0) base = atomicAdd(&sh.cnt, __popcll(mask));
                 base = __builtin_amdgcn_readfirstlane(base);
@@ -1968,7 +1988,9 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         }
         lds_barrier();
         BPH(3);
-        const int L = sh.cnt;
+        // segment path: inclusive prefix of the segment counts in every wave
+        const int seg_incl = segp ? wave_incl_int(lane_id() < nseg ? sh.segc[lane_id()] : 0) : 0;
+        const int L = segp ? __builtin_amdgcn_readlane(seg_incl, 63) : sh.cnt;
         if (dbg && tid == 0) ph_acc[11] += L;
         if (L == 0) { fail = true; break; }  // uniform: every logit -inf
         auto rnd = [&](int b) -> uint64_t {
@@ -1982,15 +2004,37 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             serial_begin();
             const int lane = lane_id();
             const bool v = lane < L;
-            const int myn = v ? lst_n[lane] : 0x7fffffff;
-            const double myl = v ? lst_l[lane] : HYG_NINF;
-            int rank = 0;
+            double sv;
+            hyg_u128* cdfa;
+            int* cn;
+            if (segp) {
+              // list position `lane` lies in the segment whose inclusive end
+              // is the first one above it
+              int seg = 0, base = 0;
+              for (int q = 0; q < nseg; ++q) {
+                const int iv = __builtin_amdgcn_readlane(seg_incl, q);
+                seg += (iv <= lane) ? 1 : 0;
+                base = (iv <= lane) ? iv : base;
+              }
+              const int at = 64 * seg + (lane - base);
+              const int myn = v ? lst_n[at] : 0;
+              sv = v ? lst_l[at] : HYG_NINF;
+              cdfa = (hyg_u128*)(Lg + 64 * kSeg);       // behind the segments
+              cn = (int*)(Lg + 64 * kSeg + 128);        // the list's indices in n order
+              if (v) cn[lane] = myn;
+            } else {
+              const int myn = v ? lst_n[lane] : 0x7fffffff;
+              const double myl = v ? lst_l[lane] : HYG_NINF;
+              int rank = 0;
 #pragma unroll 4
-            for (int j = 0; j < L; ++j) rank += (lst_n[j] < myn) ? 1 : 0;  // broadcast reads
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
-            if (v) { lst_n[rank] = myn; lst_l[rank] = myl; }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
-            const double sv = v ? lst_l[lane] : HYG_NINF;
+              for (int j = 0; j < L; ++j) rank += (lst_n[j] < myn) ? 1 : 0;  // broadcast reads
+              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+              if (v) { lst_n[rank] = myn; lst_l[rank] = myl; }
+              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+              sv = v ? lst_l[lane] : HYG_NINF;
+              cdfa = (hyg_u128*)(Lg + 64);  // behind the 64 list logits
+              cn = lst_n;
+            }
             const double lmax = wave_max(sv);
             hyg_u128 ms = hyg_u128_zero();
             if (v) ms = hyg_fix100(hyg_exp(sv - lmax));
@@ -1998,7 +2042,6 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             hyg_u128 total;
             total.lo = rdlane64(cdf.lo, L - 1);
             total.hi = rdlane64(cdf.hi, L - 1);
-            hyg_u128* cdfa = (hyg_u128*)(Lg + 64);  // behind the 64 list logits
             if (v) cdfa[lane] = cdf;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
             // lane b draws for trajectory b: first list entry with cdf > target
@@ -2010,7 +2053,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
                 const int mid = (lo + hi) >> 1;
                 if (hyg_u128_lt(tb, cdfa[mid])) hi = mid; else lo = mid + 1;
               }
-              idx[lane] = lst_n[lo];
+              idx[lane] = cn[lo];
             }
             serial_end();
           }
