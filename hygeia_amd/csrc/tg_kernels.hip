@@ -314,7 +314,7 @@ __device__ __forceinline__ uint64_t tg_xi_hz_sel(const ConstLds& cl, int K, floa
 }
 
 // ------------------------------------------------------------ LDS layout
-constexpr int kPh = 32;  // diagnostic phase timers (last entry: timestamp / step count)
+constexpr int kPh = 36;  // diagnostic phase timers (last entry: timestamp / step count)
 
 struct Shared {  // broadcast scalars of one workgroup
   double mx, logS;
@@ -1059,6 +1059,7 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
       const float l2 = (rvd == 0.0) ? HYG_NINFF : (float)hyg_log(rvd);
       ca = cl.logMa[a] - l2;
     }
+    TPH(30);
     int aa = 0, bb = -1, ovf = 0;
     while (aa != bb && aa < N && aa < M) {
       const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), aa));
@@ -1074,6 +1075,7 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
       bb = aa;
       aa = nxt > aa ? nxt : aa;
     }
+    TPH(32);
     const float lc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), bb));
     const hyg_u192 Rr = rdlane192(rva, bb);
     int status = FAST_DONE;
@@ -1106,6 +1108,7 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
       sh.log_c = lc;
       sh.fast = status;
     }
+    TPH(33);
     serial_end();
   }
   lds_barrier();
@@ -1491,6 +1494,8 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     }
     lds_barrier();
     PH(4);
+    // (np <= M <= 64 at the pipeline shape: the gather is wave 0's alone)
+    if (wave_id() == 0) serial_begin();
     // ---- gather the ancestors (state, weight, own hazards), record them,
     //      and start the hazard-row prefetch for their children
     StepScalars* rs = (StepScalars*)(rec0 + (size_t)t * rstride);
@@ -1549,6 +1554,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     if (tid == 0) {
       rs->mode = mode; rs->n_par = np; rs->log_c = log_c; rs->r_ph = 0; rs->lse = lse; rs->pad = 0.0;
     }
+    if (wave_id() == 0) serial_end();
     if (wave_id() == NT / 64 - 1) {  // a wave with no ancestor (when NT > M): next step's uniform
       const float un = hyg_u01f(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)(t + 1), 0));
       if (lane_id() == 0) sh.Unext = un;
@@ -2089,6 +2095,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     }
     lds_barrier();
     // ---- trajectories and test-function means at t (run_inference_two_groups.py:233-240, 294-314)
+    if (B <= 64 && wave_id() == 0) serial_begin();  // (ended after the means)
     for (int b = tid; b < B; b += NT) {
       const uint64_t x = state_of(idx[b]);
       X[b] = x;
@@ -2318,6 +2325,8 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
     const double opt = steps - tot[10];
     fprintf(stderr, " | topset: compact=%.0f mass=%.0f gatherA=%.0f sort=%.0f prefix=%.0f kloop_sys=%.0f",
             tot[24] / opt, tot[25] / opt, tot[26] / opt, tot[27] / opt, tot[28] / opt, tot[29] / opt);
+    fprintf(stderr, " | kloop_sys split: c(a)=%.0f loop=%.0f systematic=%.0f", tot[30] / opt, tot[32] / opt,
+            tot[33] / opt);
     fprintf(stderr, " | per optimal step: topset=%.0f fallbacks=%.4f | per fallback: hist=%.0f bscan=%.0f scatter=%.0f "
             "bsort=%.0f scan=%.0f kloop=%.0f systematic=%.0f\n", tot[20] / opt, tot[21] / opt,
             tot[17] / (tot[21] + 1e-9), tot[18] / (tot[21] + 1e-9), tot[19] / (tot[21] + 1e-9),
