@@ -2248,6 +2248,11 @@ static bool shape_specialised(const hyg_tg_consts& c) {
   static const bool off = getenv("HYG_NO_SHAPE") != nullptr;
   return !off && c.K == 6 && c.M == 50 && c.B == 25 && c.I == 48 && c.Nmax == 2400;
 }
+// the stress shape (C5: K = 12, M = 50, B = 25), one chain per CU at 512 threads
+static bool shape_c5(const hyg_tg_consts& c) {
+  static const bool off = getenv("HYG_NO_SHAPE") != nullptr;
+  return !off && c.K == 12 && c.M == 50 && c.B == 25 && c.I == 168 && c.Nmax == 8400;
+}
 // HYG_DEBUG_PHASES=1 selects the phase-timer instantiations (256 and 512 threads).
 static bool want_phases() {
   static const bool on = getenv("HYG_DEBUG_PHASES") != nullptr;
@@ -2266,6 +2271,8 @@ FwdFn fwd_kernel(const hyg_tg_consts& c) {
   }
   if constexpr (NT == 256)
     if (shape_specialised(c)) return &tg_forward_kernel<256, 6, 50, 25>;
+  if constexpr (NT == 512)
+    if (shape_c5(c)) return &tg_forward_kernel<512, 12, 50, 25>;
   return &tg_forward_kernel<NT>;
 }
 template <int NT>
@@ -2279,6 +2286,8 @@ BwdFn bwd_kernel(const hyg_tg_consts& c) {
   }
   if constexpr (NT == 256)
     if (shape_specialised(c)) return &tg_backward_kernel<256, 6, 50, 25>;
+  if constexpr (NT == 512)
+    if (shape_c5(c)) return &tg_backward_kernel<512, 12, 50, 25>;
   return &tg_backward_kernel<NT>;
 }
 
