@@ -1,0 +1,82 @@
+"""The hipcc forms of the multiword fixed-point primitives in include/hyg_arith.h
+(32-bit __builtin_addc / __builtin_subc carry chains, the forms the GPU kernels
+compile) against exact Python integers. The gcc-built oracle uses the C forms,
+which tests/test_arith.py and every oracle test exercise; together they pin
+both sides of the bit-exact contract to the same integers.
+
+The program is compiled for the host by hipcc (the same builtins and the same
+header the device code uses); no GPU is needed.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+PROG = r"""
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include "hyg_arith.h"
+static uint64_t st = 0x9E3779B97F4A7C15ull;
+static uint64_t nx() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; }
+static uint64_t word() {  // edge-heavy: 0, all ones, small, random
+  const uint64_t x = nx();
+  switch (nx() & 3) { case 0: return 0; case 1: return ~0ull; case 2: return x & 0xff; default: return x; }
+}
+int main() {
+  for (int i = 0; i < 4000; ++i) {
+    hyg_u128 a{word(), word()}, b{word(), word()};
+    if ((nx() & 7) == 0) b = a;
+    const hyg_u128 s = hyg_u128_add(a, b);
+    printf("A %016llx %016llx %016llx %016llx %016llx %016llx %d\n", (unsigned long long)a.lo,
+           (unsigned long long)a.hi, (unsigned long long)b.lo, (unsigned long long)b.hi, (unsigned long long)s.lo,
+           (unsigned long long)s.hi, hyg_u128_lt(a, b));
+    hyg_u192 x{word(), word(), word()}, y{word(), word(), word()};
+    if ((nx() & 7) == 0) y = x;
+    if ((nx() & 7) == 0) { y.w2 = x.w2; y.w1 = x.w1; }
+    const hyg_u192 z = hyg_u192_add(x, y);
+    const int ge = hyg_u192_ge(x, y);
+    const hyg_u192 d = ge ? hyg_u192_sub(x, y) : hyg_u192_sub(y, x);
+    printf("B %016llx %016llx %016llx %016llx %016llx %016llx %016llx %016llx %016llx %d %016llx %016llx %016llx\n",
+           (unsigned long long)x.w0, (unsigned long long)x.w1, (unsigned long long)x.w2, (unsigned long long)y.w0,
+           (unsigned long long)y.w1, (unsigned long long)y.w2, (unsigned long long)z.w0, (unsigned long long)z.w1,
+           (unsigned long long)z.w2, ge, (unsigned long long)d.w0, (unsigned long long)d.w1,
+           (unsigned long long)d.w2);
+  }
+  return 0;
+}
+"""
+
+
+def _join(words):
+    return sum(int(w, 16) << (64 * i) for i, w in enumerate(words))
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_carry_chain_forms_match_exact_integers(tmp_path):
+    src = tmp_path / "carry.hip"
+    exe = tmp_path / "carry"
+    src.write_text(PROG)
+    subprocess.run([HIPCC, "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"), "-o", str(exe), str(src)],
+                   check=True, capture_output=True, timeout=300)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True, timeout=60).stdout.split("\n")
+    n128 = n192 = 0
+    for line in out:
+        f = line.split()
+        if not f:
+            continue
+        if f[0] == "A":
+            a, b, s = _join(f[1:3]), _join(f[3:5]), _join(f[5:7])
+            assert s == (a + b) % (1 << 128)
+            assert int(f[7]) == int(a < b)
+            n128 += 1
+        else:
+            x, y, z = _join(f[1:4]), _join(f[4:7]), _join(f[7:10])
+            assert z == (x + y) % (1 << 192)
+            assert int(f[10]) == int(x >= y)
+            assert _join(f[11:14]) == abs(x - y)
+            n192 += 1
+    assert n128 == 4000 and n192 == 4000
