@@ -1116,6 +1116,24 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
   return sh.fast;
 }
 
+// hyg_fix149f for masses m < 2^-21 (image m 2^149 < 2^128): the two low words
+// of the same integer, the 24-bit significand shifted by E - 1 <= 105.
+__device__ __forceinline__ hyg_u128 fix149f_low128(float m) {
+  const uint32_t b = hyg_f32_bits(m);
+  const int E = (int)((b >> 23) & 0xff);
+  const uint64_t man = b & 0x7fffffu;
+  const uint64_t v = (E == 0) ? man : (man | 0x800000u);
+  const int sh = (E == 0) ? 0 : E - 1;
+  const int s0 = sh & 63;
+  const uint64_t lo = v << s0;
+  const uint64_t hi = (v >> 1) >> (63 - s0);  // v >> (64 - s0), 0 for s0 = 0
+  const bool zero = (b == 0) || (b >> 31);
+  hyg_u128 r;
+  r.lo = (zero || sh >= 64) ? 0 : lo;
+  r.hi = zero ? 0 : ((sh < 64) ? hi : lo);
+  return r;
+}
+
 // Top-set path of OptimalFiniteState; returns FAST_DONE (parents / Kk /
 // log_c written; log_c infinite -> the caller's unbiased fallback),
 // FAST_FALLBACK (W intact) or FAST_FALLBACK_REGEN (W overwritten). The
@@ -1151,8 +1169,14 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
   const double cutx = (ks == kNCut - 1) ? HYG_NINF : -cut_below_top(ks);
   int off = 0;
   for (int w = 0; w < wv; ++w) off += __builtin_amdgcn_readlane(pc, w * kNCut + ks);
-  // ---- 2. gather A's keys; exact mass of the list weights outside A
+  // ---- 2. gather A's keys; exact mass of the list weights outside A. From the
+  // third cutoff on (X >= 20 nats below the top: every outside mass is below
+  // e^-20 < 2^-28.8, its image m 2^149 below 2^120.2, and a lane sums at most
+  // ceil(N / NT) <= 128 of them, below 2^127.2) a lane's images are formed and
+  // summed as u128.
+  const bool narrow = ks >= 2 && (N + NT - 1) / NT <= 128;
   hyg_u192 mb = hyg_u192_zero(), mb2 = hyg_u192_zero();
+  hyg_u128 nb = hyg_u128_zero(), nb2 = hyg_u128_zero();
   for (int b = 0; b < cw; b += 64 * kLR) {  // kLR entries per lane, loads first (see the lse loop)
     int nn[kLR];
     float lw[kLR];
@@ -1176,7 +1200,14 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
       if (inA[r]) srt[off + lanes_below(bal)] = sort_key(lw[r], nn[r]);
       off += (int)__builtin_popcountll(bal);
     }
-    if (hasB) {  // uniform; expf(lw) is 0 below sig_thresh
+    if (hasB && narrow) {  // uniform; expf(lw) is 0 below sig_thresh
+#pragma unroll
+      for (int r = 0; r < kLR; ++r) {
+        const float m = hyg_expf(lw[r]);
+        const hyg_u128 f = fix149f_low128(outA[r] ? m : 0.0f);
+        if (r & 1) nb2 = hyg_u128_add(nb2, f); else nb = hyg_u128_add(nb, f);
+      }
+    } else if (hasB) {
 #pragma unroll
       for (int r = 0; r < kLR; ++r) {
         const float m = hyg_expf(lw[r]);
@@ -1185,8 +1216,13 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
       }
     }
   }
-  mb = hyg_u192_add(mb, mb2);
   if (hasB) {
+    if (narrow) {
+      const hyg_u128 t = hyg_u128_add(nb, nb2);
+      mb.w0 = t.lo; mb.w1 = t.hi; mb.w2 = 0;
+    } else {
+      mb = hyg_u192_add(mb, mb2);
+    }
     const hyg_u192 ws = wave_sum192(mb);
     if (lane == 0) part_tot[wv] = ws;
   }
