@@ -3,7 +3,7 @@
 Default workload (BASELINE.json configs[2], "C3"): two-group, 28M CpG over 22
 chromosomes cut into the reference's 100k-site segments with 5k buffers
 (run_inference_two_groups.py:194-218), 4 + 4 samples, K = 6, M = 50, B = 25,
-2 inference seeds per GPU. One "step" = the whole hot path over that workload
+2 inference seeds. One "step" = the whole hot path over that workload
 with the counts resident in HBM: Beta-Binomial emission table, particle filter
 with optimal finite-state resampling, backward simulation of 25 trajectories,
 for every (chromosome segment, seed) chain, then the job's gather: per-site
@@ -11,13 +11,16 @@ posterior counts over all trajectories, summed over ranks by one RCCL
 all-reduce (hygeia_amd/parallel.py; aggregate_results.py:129,181).
 Units = trimmed CpG sites x seeds.
 
-Jobs (--job):
-  c3  (default) weak scaling: every rank runs the whole genome for its own
-      --seeds seeds (no data-path collective);
-  c4  strong scaling: ONE fixed job of --total-seeds (8) seeds; the chain list
-      chrom x segment x seed (main.nf:46-75, modules/two_group/4_infer.nf:28) is
-      split over the ranks longest-first by parallel.shard_chains;
-  c5  the stress config: 50 + 50 samples, K = 12, 4 seeds per GPU (weak).
+Jobs (--job); every job is ONE fixed job whose chain list chrom x segment x
+seed (main.nf:46-75, modules/two_group/4_infer.nf:28) is split over the ranks
+longest-first by parallel.shard_chains (strong scaling, no data-path
+collective; the final all-reduce of the posterior counts is the gather):
+  c3  (default) the metric's job: 2 seeds (BASELINE.json configs[2]; at 1/2/4/8
+      GPUs the same 582 chains);
+  c4  --total-seeds (8) seeds (configs[3]);
+  c5  the stress config: 50 + 50 samples, K = 12, 4 seeds (configs[4]).
+A rehearsal of several ranks on fewer GPUs (--dist-backend gloo) reports the
+GPUs it used in n_gpus and the ranks in "ranks".
 
 Also reported: the roofline of the dominant kernel (HIP events on the launch
 stream), the HBM traffic and VALU-issue fraction from the PMC passes of the same
@@ -191,18 +194,19 @@ def pmc_record(name: str, workload: str):
     return rec
 
 
+def job_seeds(args) -> int:
+    """Inference seeds of the whole (fixed) job."""
+    return args.total_seeds if args.job == "c4" else args.seeds
+
+
 def build_chains(args, segs, rank, world):
     """This rank's chains (site_begin, n_sites, seed, chain_id, out_begin), the
     units (trimmed site-seeds) it processes, and the seeds it uses."""
-    if args.job == "c4":
-        allc = [(seg, sd) for sd in range(args.total_seeds) for seg in segs]
-        from hygeia_amd import parallel
+    from hygeia_amd import parallel
 
-        mine = parallel.shard_chains([c[0][3] for c in allc], world)[rank]
-        picked = [allc[i] for i in mine]
-    else:
-        seeds = [rank * args.seeds + s for s in range(args.seeds)]
-        picked = [(seg, sd) for sd in seeds for seg in segs]
+    allc = [(seg, sd) for sd in range(job_seeds(args)) for seg in segs]
+    mine = parallel.shard_chains([c[0][3] for c in allc], world)[rank]
+    picked = [allc[i] for i in mine]
     chains, out, units = [], 0, 0
     for (ci, b, s0, n, r0, rl), sd in picked:
         chains.append((s0, n, sd, (ci << 32) | b, out))
@@ -219,7 +223,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--job", choices=("c3", "c4", "c5"), default="c3")
     ap.add_argument("--sites", type=int, default=28_000_000)
-    ap.add_argument("--seeds", type=int, default=None, help="inference seeds per GPU (c3/c5)")
+    ap.add_argument("--seeds", type=int, default=None, help="inference seeds of the c3 / c5 job")
     ap.add_argument("--total-seeds", type=int, default=8, help="seeds of the fixed c4 job")
     ap.add_argument("--samples", type=int, default=None, help="samples per group")
     ap.add_argument("--K", type=int, default=None)
@@ -230,6 +234,9 @@ def main():
     ap.add_argument("--history-gib", type=float, default=100.0, help="forward->backward history budget in HBM")
     ap.add_argument("--launch-chains", type=int, default=768, help="chains per launch when over the budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", default=None, metavar="R/W",
+                    help="run only rank R's chains of a W-rank job on this one GPU (a projection of one rank of "
+                         "a W-GPU run; the line is labelled as such)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm); gloo rehearses the multi-rank path, e.g. 2 ranks on one GPU")
     args = ap.parse_args()
@@ -262,7 +269,13 @@ def main():
                                      device=dev)
     sizes = synthetic.chromosome_sizes(args.sites)
     segs = synthetic.segment_chains(sizes)
-    chains, n_out, units, picked = build_chains(args, segs, rank, world)
+    if args.shard:
+        if world > 1:
+            raise SystemExit("--shard is a single-process projection")
+        srank, sworld = (int(x) for x in args.shard.split("/"))
+        chains, n_out, units, picked = build_chains(args, segs, srank, sworld)
+    else:
+        chains, n_out, units, picked = build_chains(args, segs, rank, world)
     max_reads = int(max(data["tot_control"].to(torch.int32).max().item() & 0xFFFF,
                         data["tot_case"].to(torch.int32).max().item() & 0xFFFF))
     mu, sg = synthetic.regime_params(K)
@@ -335,9 +348,12 @@ def main():
     if (status != 0).any():
         raise RuntimeError(f"{int((status != 0).sum())} chains failed: {np.unique(status)}")
     # every site is counted once per trajectory of every seed of the job
-    seeds_job = args.total_seeds if args.job == "c4" else args.seeds * world
+    seeds_job = job_seeds(args)
     per_site = counts[:, 1:1 + K].sum(dim=1)
-    if not bool((per_site == B * seeds_job).all().item()):
+    if args.shard:  # this rank's trimmed sites, once per trajectory of their chains' seeds
+        if int(per_site.sum().item()) != B * units:
+            raise RuntimeError("posterior counts do not cover the shard's sites once per trajectory")
+    elif not bool((per_site == B * seeds_job).all().item()):
         raise RuntimeError("posterior counts do not cover every site once per trajectory of every seed")
     total_units = units
     if dist:
@@ -360,8 +376,7 @@ def main():
         cfg_name = "custom"
     workload = (f"{cfg_name} two_group {args.sites} CpG (22 chromosomes, 100k segments + 5k buffers), "
                 f"{args.samples}+{args.samples} samples, K={K}, M={M}, B={B}, "
-                + (f"{args.total_seeds} seeds in total, chains sharded over the GPUs (LPT)" if args.job == "c4"
-                   else f"{args.seeds} seeds per GPU"))
+                f"{job_seeds(args)} seeds in total, chains sharded over the GPUs (LPT)")
     tr = pmc_record("traffic", workload) if world == 1 else None
     iss = pmc_record("issue", workload) if world == 1 else None
     roof = {"bound": "hbm", "kernel": names[dom], "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -374,16 +389,24 @@ def main():
         roof["issue"] = {"valu_wave_instr_per_s": rate, "peak": N_SIMD * clk / VALU_ISSUE_CYCLES,
                          "clock_hz": clk, "frac": rate / (N_SIMD * clk / VALU_ISSUE_CYCLES),
                          "source": f"profiles/pmc_issue.json (SQ_INSTS_VALU, GRBM_GUI_ACTIVE; build {iss['source_hash']})"}
+    n_gpus = min(world, torch.cuda.device_count())  # a gloo rehearsal may put several ranks on one GPU
     line = {
-        "metric": METRIC, "value": value, "unit": "CpG-sites*seeds/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC, "value": value, "unit": "CpG-sites*seeds/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-        "scaling": "strong" if args.job == "c4" else "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": workload, "chains_per_gpu": len(chains), "launches_per_step": len(runs),
+        "config": {"workload": workload, "chains_per_rank": len(chains), "launches_per_step": len(runs),
+                   "threads_per_chain": int(L.hyg_tg_threads_per_chain(model.handle, len(chains))),
                    "global_sites_x_seeds": total_units,
-                   "parallelism": f"chains over {world} GPU(s)"},
+                   "parallelism": f"chains over {world} rank(s) on {n_gpus} GPU(s)"},
         "roofline": roof,
     }
+    if args.shard:
+        line["projection"] = (f"one GPU running rank {srank}'s chains of a {sworld}-rank job: value = that rank's "
+                              f"units / its time, NOT the job's throughput")
+    if world != n_gpus:
+        line["ranks"] = world
+        line["rehearsal"] = f"{world} {args.dist_backend} ranks on {n_gpus} GPU(s)"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host = {k: data[k].cpu().numpy().view(np.uint16) for k in
                 ("meth_control", "tot_control", "meth_case", "tot_case")}

@@ -7,6 +7,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -100,6 +103,41 @@ struct PinnedStage {
   }
 };
 
+// One pinned stage per stream, each behind its own mutex: host threads that
+// share a model on different streams neither race on a buffer nor wait for
+// each other's kernels (an upload waits only for the previous upload of its
+// own stream); two threads on one stream take turns.
+class PinnedStages {
+ public:
+  hipError_t upload(void* dst, const void* src, size_t n, hipStream_t s) {
+    Slot* slot;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      std::unique_ptr<Slot>& u = by_stream_[s];
+      if (!u) u.reset(new Slot);
+      slot = u.get();
+    }
+    std::lock_guard<std::mutex> g(slot->mu);
+    return slot->st.upload(dst, src, n, s);
+  }
+  void release() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : by_stream_) {
+      std::lock_guard<std::mutex> gs(kv.second->mu);
+      kv.second->st.release();
+    }
+    by_stream_.clear();
+  }
+
+ private:
+  struct Slot {
+    std::mutex mu;
+    PinnedStage st;
+  };
+  std::mutex mu_;
+  std::map<hipStream_t, std::unique_ptr<Slot>> by_stream_;
+};
+
 }  // namespace
 
 struct hyg_tg_model {
@@ -115,7 +153,7 @@ struct hyg_tg_model {
   double* d_lf = nullptr;
   double* d_lg = nullptr;
   double* d_cst = nullptr;
-  mutable PinnedStage stage;  // descriptor uploads (a model is used by one thread at a time)
+  mutable PinnedStages stage;  // descriptor uploads (thread-safe, one pinned buffer per stream)
 
   ModelDev dev() const {
     ModelDev m{};
@@ -140,7 +178,7 @@ struct hyg_sg_model {
   std::vector<uint8_t> ex;
   bool on_device = false;
   int device = -1;
-  mutable PinnedStage stage;  // descriptor uploads (a model is used by one thread at a time)
+  mutable PinnedStages stage;  // descriptor uploads (thread-safe, one pinned buffer per stream)
   hyg_sg_consts* d_consts = nullptr;
   double* d_hz = nullptr;
   uint8_t* d_ex = nullptr;
@@ -256,6 +294,10 @@ int hyg_tg_model_create(const hyg_tg_params* params, int32_t max_total_reads, in
 }
 
 int32_t hyg_tg_num_particles(const hyg_tg_model* m) { return m ? m->c.Nmax : 0; }
+
+int32_t hyg_tg_threads_per_chain(const hyg_tg_model* m, int32_t n_chains) {
+  return m ? hyg::tg_threads_per_chain(m->c, n_chains) : 0;
+}
 
 int hyg_tg_emission(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_t* tot_c, int32_t s_c,
                     const uint16_t* meth_k, const uint16_t* tot_k, int32_t s_k, int64_t n_sites, double* E,

@@ -233,6 +233,65 @@ __device__ __forceinline__ int wave_incl_int(int v) {
   return (int)x;
 }
 
+// ---- combining the per-wave partials of a block reduction
+// Up to 4 waves: every lane reads all of them from LDS (broadcast reads) and
+// adds them in wave order. More waves (384 / 768-thread chains): lane l < NW
+// reads wave l's partial and a DPP row reduction / scan combines them, so the
+// registers and instructions do not grow with the workgroup (NW <= 16).
+template <int CTRL>
+__device__ __forceinline__ hyg_u192 dpp192f(hyg_u192 v) {
+  hyg_u192 r;
+  r.w0 = dpp64<CTRL>(v.w0); r.w1 = dpp64<CTRL>(v.w1); r.w2 = dpp64<CTRL>(v.w2);
+  return r;
+}
+__device__ __forceinline__ hyg_u192 row_sum192(hyg_u192 v) {  // every lane of a row: the row's sum
+  v = hyg_u192_add(v, dpp192f<kDppQuad1032>(v));
+  v = hyg_u192_add(v, dpp192f<kDppQuad2301>(v));
+  v = hyg_u192_add(v, dpp192f<kDppRowHalfMirror>(v));
+  v = hyg_u192_add(v, dpp192f<kDppRowMirror>(v));
+  return v;
+}
+__device__ __forceinline__ hyg_u128 row_sum128(hyg_u128 v) {
+  hyg_u128 w;
+  w.lo = dpp64<kDppQuad1032>(v.lo); w.hi = dpp64<kDppQuad1032>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppQuad2301>(v.lo); w.hi = dpp64<kDppQuad2301>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppRowHalfMirror>(v.lo); w.hi = dpp64<kDppRowHalfMirror>(v.hi); v = hyg_u128_add(v, w);
+  w.lo = dpp64<kDppRowMirror>(v.lo); w.hi = dpp64<kDppRowMirror>(v.hi); v = hyg_u128_add(v, w);
+  return v;
+}
+template <int NW>
+__device__ __forceinline__ hyg_u192 sum_waves192(const hyg_u192* r) {
+  static_assert(NW >= 1 && NW <= 16, "waves per workgroup");
+  if constexpr (NW <= 4) {
+    hyg_u192 s = r[0];
+    for (int w = 1; w < NW; ++w) s = hyg_u192_add(s, r[w]);
+    return s;
+  } else {
+    const int l = lane_id();
+    hyg_u192 v = hyg_u192_zero();
+    if (l < NW) v = r[l];
+    return rdlane192(row_sum192(v), 0);
+  }
+}
+template <int NW>
+__device__ __forceinline__ hyg_u128 sum_waves128(const hyg_u128* r) {
+  static_assert(NW >= 1 && NW <= 16, "waves per workgroup");
+  if constexpr (NW <= 4) {
+    hyg_u128 s = r[0];
+    for (int w = 1; w < NW; ++w) s = hyg_u128_add(s, r[w]);
+    return s;
+  } else {
+    const int l = lane_id();
+    hyg_u128 v = hyg_u128_zero();
+    if (l < NW) v = r[l];
+    v = row_sum128(v);
+    hyg_u128 o;
+    o.lo = rdlane64(v.lo, 0);
+    o.hi = rdlane64(v.hi, 0);
+    return o;
+  }
+}
+
 // Block-wide reductions. `red` is an LDS scratch of at least 32 B per wave;
 // every call starts with a barrier so consecutive calls may reuse it
 // (LEAD = false: the caller guarantees that every read of `red` by an earlier
@@ -248,14 +307,32 @@ __device__ __forceinline__ void block_max_cnt(double m, int c, unsigned char* re
     ((int*)red)[4 * wave_id() + 2] = c;
   }
   lds_barrier();
-  double mm = ((double*)red)[0];
-  int cc = ((int*)red)[2];
-  for (int w = 1; w < NT / 64; ++w) {
-    mm = dmax(mm, ((double*)red)[2 * w]);
-    cc += ((int*)red)[4 * w + 2];
+  if constexpr (NT / 64 <= 4) {
+    double mm = ((double*)red)[0];
+    int cc = ((int*)red)[2];
+    for (int w = 1; w < NT / 64; ++w) {
+      mm = dmax(mm, ((double*)red)[2 * w]);
+      cc += ((int*)red)[4 * w + 2];
+    }
+    *m_out = mm;
+    *c_out = cc;
+  } else {
+    const int l = lane_id();
+    double mm = HYG_NINF;
+    uint32_t cc = 0;
+    if (l < NT / 64) {
+      mm = ((double*)red)[2 * l];
+      cc = (uint32_t)((int*)red)[4 * l + 2];
+    }
+    auto mx = [](double a, double b) { return dmax(a, b); };
+    mm = row_reduce_d(mm, mx);
+    cc += dpp32<kDppQuad1032>(cc);
+    cc += dpp32<kDppQuad2301>(cc);
+    cc += dpp32<kDppRowHalfMirror>(cc);
+    cc += dpp32<kDppRowMirror>(cc);
+    *m_out = d_of(rdlane64(u_of(mm), 0));
+    *c_out = __builtin_amdgcn_readlane((int)cc, 0);
   }
-  *m_out = mm;
-  *c_out = cc;
 }
 template <int NT>
 __device__ __forceinline__ double block_max(double v, unsigned char* red) {
@@ -264,9 +341,15 @@ __device__ __forceinline__ double block_max(double v, unsigned char* red) {
   lds_barrier();
   if (lane_id() == 0) ((double*)red)[wave_id()] = v;
   lds_barrier();
-  double m = ((double*)red)[0];
-  for (int w = 1; w < NT / 64; ++w) m = dmax(m, ((double*)red)[w]);
-  return m;
+  if constexpr (NT / 64 <= 4) {
+    double m = ((double*)red)[0];
+    for (int w = 1; w < NT / 64; ++w) m = dmax(m, ((double*)red)[w]);
+    return m;
+  } else {
+    const double m = lane_id() < NT / 64 ? ((double*)red)[lane_id()] : HYG_NINF;
+    auto mx = [](double a, double b) { return dmax(a, b); };
+    return d_of(rdlane64(u_of(row_reduce_d(m, mx)), 0));
+  }
 }
 template <int NT, bool LEAD = true>
 __device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red) {
@@ -276,9 +359,7 @@ __device__ __forceinline__ hyg_u128 block_sum128(hyg_u128 v, unsigned char* red)
   if constexpr (LEAD) lds_barrier();
   if (lane_id() == 0) r[wave_id()] = v;
   lds_barrier();
-  hyg_u128 s = hyg_u128_zero();
-  for (int w = 0; w < NT / 64; ++w) s = hyg_u128_add(s, r[w]);
-  return s;
+  return sum_waves128<NT / 64>(r);
 }
 
 // Block-wide OR of a predicate through LDS (no vmcnt drain, unlike
@@ -308,9 +389,18 @@ __device__ __forceinline__ hyg_u192 block_excl192(hyg_u192 v, unsigned char* red
   if (lane_id() == 0) r[wave_id()] = wt;
   lds_barrier();
   hyg_u192 pre = hyg_u192_zero(), tot = hyg_u192_zero();
-  for (int w = 0; w < NT / 64; ++w) {
-    if (w < wave_id()) pre = hyg_u192_add(pre, r[w]);
-    tot = hyg_u192_add(tot, r[w]);
+  if constexpr (NT / 64 <= 4) {
+    for (int w = 0; w < NT / 64; ++w) {
+      if (w < wave_id()) pre = hyg_u192_add(pre, r[w]);
+      tot = hyg_u192_add(tot, r[w]);
+    }
+  } else {  // lane l: waves 0..l inclusive; this wave's prefix at lane wave - 1
+    const int l = lane_id(), wv = wave_id();
+    hyg_u192 x = hyg_u192_zero();
+    if (l < NT / 64) x = r[l];
+    x = wave_incl192(x);
+    tot = rdlane192(x, NT / 64 - 1);
+    if (wv > 0) pre = rdlane192(x, wv - 1);
   }
   *total = tot;
   return hyg_u192_add(pre, hyg_u192_sub(inc, v));
@@ -341,9 +431,22 @@ __device__ __forceinline__ void block_scan128(hyg_u128 v, hyg_u128* out, unsigne
   if (lane_id() == 0) r[wave_id()] = wt;
   lds_barrier();
   hyg_u128 pre = hyg_u128_zero(), tot = hyg_u128_zero();
-  for (int w = 0; w < NT / 64; ++w) {
-    if (w < wave_id()) pre = hyg_u128_add(pre, r[w]);
-    tot = hyg_u128_add(tot, r[w]);
+  if constexpr (NT / 64 <= 4) {
+    for (int w = 0; w < NT / 64; ++w) {
+      if (w < wave_id()) pre = hyg_u128_add(pre, r[w]);
+      tot = hyg_u128_add(tot, r[w]);
+    }
+  } else {
+    const int l = lane_id(), wv = wave_id();
+    hyg_u128 x = hyg_u128_zero();
+    if (l < NT / 64) x = r[l];
+    x = wave_incl128(x);
+    tot.lo = rdlane64(x.lo, NT / 64 - 1);
+    tot.hi = rdlane64(x.hi, NT / 64 - 1);
+    if (wv > 0) {
+      pre.lo = rdlane64(x.lo, wv - 1);
+      pre.hi = rdlane64(x.hi, wv - 1);
+    }
   }
   hyg_u128 e2;  // inc - v
   e2.lo = inc.lo - v.lo;

@@ -71,7 +71,8 @@ constexpr int kSgRing = 32;
 __host__ __device__ inline size_t sg_rec_bytes(int K) {
   return (16 + 8 * 2 * (size_t)kSgThreads + 8 * (size_t)K * kSgThreads + 255) / 256 * 256;
 }
-constexpr size_t kSgCtlBytes = 16;  // per chain: head (records published), tail (consumed), abort code, pad
+constexpr size_t kSgCtlBytes = 16;  // per chain: head (records published), tail (consumed), abort code, and
+                                    // (first chain of a launch) the launch's dispatch-ticket counter
 
 // Per-chain workspace: cap psi slots [K][256] f64, then the pending-time lists
 // slot[2][cap] / time[2][cap] (double-buffered), keep[cap], free[cap] (int32),

@@ -203,6 +203,11 @@ typedef __attribute__((address_space(1))) unsigned int sg_gu32;
 typedef __attribute__((address_space(1))) unsigned long long sg_gu64;
 constexpr unsigned kSgTailAbort = 0x7fffffffu;  // the smoothing workgroup gave up: never wait for ring space
 constexpr unsigned kSgSpinMax = 1u << 24;       // bounded spins (~25 s of polling): then HYG_EDEVICE
+// the first record may wait for the SMC workgroup to become resident, i.e. for
+// another chain of a crowded GPU to finish (a chromosome-1 chain: ~35 s)
+constexpr unsigned kSgSpinFirst = 1u << 26;
+// ctl word 3 of a launch's first chain: the launch's dispatch-ticket counter
+constexpr size_t kSgTicketOffset = 12;
 __device__ __forceinline__ void sg_st8(uint8_t* p, uint64_t v) {
   __hip_atomic_store((sg_gu64*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -431,17 +436,29 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
                 SgLay lay, SgCLay clay, unsigned long long* __restrict__ dbg_arg, SgPeDev pe) {
   // a constant null pointer outside the timer build: every timer test folds away
   unsigned long long* __restrict__ const dbg = PHS ? dbg_arg : nullptr;
-  // blocks [0, n_chains): the SMC of chain b; blocks [n_chains, 2 n_chains):
-  // the online marginal smoothing of chain b - n_chains, fed by the ring
-  if ((int)blockIdx.x >= n_chains) {
-    const int chain = (int)blockIdx.x - n_chains;
+  // Roles by dispatch ticket, not by block index: the k-th workgroup to start
+  // takes ticket k; ticket 2c is the online marginal smoothing of chain c,
+  // ticket 2c + 1 its SMC, fed through the ring. A chain's two workgroups wait
+  // for each other, so both must be resident at once. With tickets taken in
+  // the order workgroups actually become resident, at most one resident
+  // workgroup (a smoothing one, which only polls) waits for a partner that is
+  // not resident yet, and every other resident pair runs to completion and
+  // frees its CUs: the launch finishes whenever two workgroups fit on the GPU,
+  // whatever else shares it (other streams, other processes, CU masks).
+  __shared__ int role_ticket;
+  if (threadIdx.x == 0)
+    role_ticket = (int)__hip_atomic_fetch_add((sg_gu32*)(ws + chains[0].ctl_offset + kSgTicketOffset), 1u,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int chain = role_ticket >> 1;
+  if ((role_ticket & 1) == 0) {
     sg_smoother<KT, NB>(md, chains[chain], chain, ws, cap, probs, status_out, clay);
     return;
   }
   constexpr int NT = kSgThreads, NW = NB / 64, K = KT;  // NT: particle slots, NB: threads
   const hyg_sg_consts& c = *md.consts;
   const int Nmax = c.Nmax, u = c.u, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const SgChainDev ch = chains[blockIdx.x];
+  const SgChainDev ch = chains[chain];
   const int T = ch.T;
   uint8_t* ring = ws + ch.ring_offset;
   uint8_t* ctl = ws + ch.ctl_offset;
@@ -530,7 +547,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
   int fin;
   block_max_cnt<NB>(my_lw, (tid < K && hyg_isfinite(my_lw)) ? 1 : 0, red, &mx0, &fin);
   if (!(mx0 > HYG_NINF)) {
-    if (tid == 0) status_out[blockIdx.x] = HYG_ENUMERIC;
+    // no finite initial weight: publish the abort code as the post-loop path
+    // does, so the smoothing workgroup stops at once and writes the status
+    if (tid == 0) sg_st4(ctl + 8, (unsigned)(-HYG_ENUMERIC));
     return;
   }
   double logZ =
@@ -1095,8 +1114,8 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
     else sg_st4(ctl + 8, (unsigned)(-status));
   }
 
-  if (dbg && tid < 15) dbg[(size_t)blockIdx.x * 16 + tid] = sh.ph[tid];
-  if (dbg && tid == 15) dbg[(size_t)blockIdx.x * 16 + 15] = (unsigned long long)T;
+  if (dbg && tid < 15) dbg[(size_t)chain * 16 + tid] = sh.ph[tid];
+  if (dbg && tid == 15) dbg[(size_t)chain * 16 + 15] = (unsigned long long)T;
 #undef SG_PH
 #undef SG_CNT
 }
@@ -1166,7 +1185,7 @@ __device__ __forceinline__ void sg_smoother(const SgModelDev md, const SgChainDe
           h = sg_ld4(ctl);
           ab = sg_ld4(ctl + 8);
           if ((int)h > t || ab != 0) break;
-          if (++spins > kSgSpinMax) { ab = (unsigned)(-HYG_EDEVICE); break; }
+          if (++spins > (t == 0 ? kSgSpinFirst : kSgSpinMax)) { ab = (unsigned)(-HYG_EDEVICE); break; }
           __builtin_amdgcn_s_sleep(2);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1372,9 +1391,11 @@ __device__ __forceinline__ void sg_smoother(const SgModelDev md, const SgChainDe
 }
 
 // ------------------------------------------------------------- launches
-// One launch per group of at most (CUs / 2) chains: the SMC and the smoothing
-// workgroup of every chain must be co-resident (one workgroup per CU at this
-// LDS size), since each waits for the other through the ring.
+// One launch per group of at most (resident workgroups / 2) chains, from the
+// occupancy query: on an otherwise idle GPU every chain's SMC and smoothing
+// workgroups are then resident together and nothing waits for a CU. The
+// dispatch tickets (sg_chain_kernel) keep a crowded GPU correct too: a pair
+// only waits for a CU to free up.
 template <int KT, int NB, bool PE, bool PHS = false>
 static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, int n_chains, const double* E,
                             uint8_t* ws, int cap, double* probs, int32_t* status, const SgLay& lay,
@@ -1386,7 +1407,11 @@ static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, 
   int dev = 0, cus = 0;
   if ((*err = hipGetDevice(&dev)) != hipSuccess) return;
   if ((*err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return;
-  const int per = cus / 2 > 0 ? cus / 2 : 1;
+  int nb = 0;
+  if ((*err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sg_chain_kernel<KT, NB, PE, PHS>, NB,
+                                                          lds)) != hipSuccess)
+    return;
+  const int per = nb * cus / 2 > 0 ? nb * cus / 2 : 1;
   for (int c0 = 0; c0 < n_chains; c0 += per) {
     const int nc = (n_chains - c0) < per ? (n_chains - c0) : per;
     hipLaunchKernelGGL((sg_chain_kernel<KT, NB, PE, PHS>), dim3(2 * nc), dim3(NB), lds, s, md, chains_dev + c0, nc, E,

@@ -11,6 +11,9 @@ namespace hyg {
 
 constexpr int kDefaultThreads = 256;     // forward workgroup size
 constexpr int kDefaultThreadsBwd = 256;  // backward workgroup size (HYG_THREADS[_FWD/_BWD] override)
+// forward / backward workgroup size when a launch has at most one chain per CU
+// (tg_kernels.hip threads_per_chain; HYG_LOWOCC_THREADS overrides the forward's)
+constexpr int kLowOccThreads = 768;
 constexpr int kEBlock = 8;     // emission rows staged in LDS per block of steps
 
 // Device-side chain descriptor (lives in the workspace header).
@@ -62,9 +65,10 @@ int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* 
                     double* E, void* stream);
 int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
                   const double* E, uint8_t* ws, const hyg_tg_outputs& out, void* stream);
-size_t forward_lds_bytes(const hyg_tg_consts& c);
+size_t forward_lds_bytes(const hyg_tg_consts& c, int n_chains);
 void set_kernel_timing(bool on);
 int last_kernel_ms(float* out3);
-size_t backward_lds_bytes(const hyg_tg_consts& c);
+size_t backward_lds_bytes(const hyg_tg_consts& c, int n_chains);
+int tg_threads_per_chain(const hyg_tg_consts& c, int n_chains);  // forward workgroup size of a launch
 
 }  // namespace hyg

@@ -336,7 +336,18 @@ __host__ __device__ inline int next_pow2(int x) {
 
 constexpr int kBuckets = 512;  // counting-sort buckets of the resampling sort (sqrt-spaced in -lw)
 constexpr int kNCut = 8;       // log-weight cutoffs of the top-set resampling path
-constexpr int kLR = 4;         // candidate-list entries per lane per chunk (lse / top-set gather)
+// candidate-list entries per lane per chunk (lse / top-set gather): ~900 list
+// entries at C3 are ~3.5 per lane at 256 threads, under one at 1024
+template <int NT>
+constexpr int kLRof = NT >= 512 ? 2 : 4;
+// waves that sort the top set A: at most 256 keys (one per lane of 4 waves)
+// whatever the workgroup size, so a 512- or 1024-thread chain sorts no more
+// keys than a 256-thread one (HYG_SORT_WAVES overrides, for tuning builds)
+#ifndef HYG_SORT_WAVES
+#define HYG_SORT_WAVES 4
+#endif
+template <int NT>
+constexpr int kSortWaves = (NT / 64 < HYG_SORT_WAVES) ? NT / 64 : HYG_SORT_WAVES;
 
 struct Lay {  // byte offsets into the dynamic LDS (32-bit: one SGPR each in the kernels)
   uint32_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, rb, red, sh,
@@ -919,11 +930,20 @@ enum { FAST_DONE = 0, FAST_FALLBACK = 1, FAST_FALLBACK_REGEN = 2 };
 
 // cutoffs of the top set in W - mx (nats below the largest weight); the last
 // set (k = kNCut - 1) is the whole candidate list (W - mx >= sig_thresh)
-__device__ __forceinline__ double cut_below_top(int k) {
+__host__ __device__ constexpr double cut_below_top(int k) {
   // selects, not a table: a runtime index into a local array is a memory load
   return k < 4 ? (k < 2 ? (k == 0 ? 14.0 : 17.0) : (k == 2 ? 20.0 : 23.0))
                : (k < 6 ? (k == 4 ? 26.0 : 30.0) : 36.0);
 }
+
+// The narrow (u128) images of the top set's outside masses: from cutoff
+// kNarrowCut on, every outside mass is below e^-cut, and a lane sums at most
+// kNarrowPerLane of them; their images m 2^149 must sum below 2^128, i.e.
+// cut > ln(kNarrowPerLane 2^21) = 19.41 nats for 128 entries per lane.
+constexpr int kNarrowCut = 2;
+constexpr int kNarrowPerLane = 128;
+static_assert(kNarrowPerLane <= 128 && cut_below_top(kNarrowCut) >= 19.5,
+              "u128 outside-mass images: 128 masses below e^-19.5 sum below 2^128 at scale 2^149");
 
 // Lanes l of a wave whose key keeps the minimum at stage (KK, J) of the
 // bitonic sort below, for J in [R, 64R) and the wave bit of i clear
@@ -994,31 +1014,55 @@ struct Bitonic {
     else if constexpr (KK < 64 * (NT / 64) * R) Bitonic<NT, R, 2 * KK, KK>::run(e, buf, ib);
   }
 };
+// workgroup barriers of a bitonic sort of n keys held R per lane (one per
+// cross-wave stage): the waves of a larger workgroup that take no part in the
+// sort pass the same number of barriers
+constexpr int bitonic_lds_stages(int n, int R) {
+  int c = 0;
+  for (int kk = 2; kk <= n; kk *= 2)
+    for (int j = kk / 2; j >= 1; j /= 2) c += (j >= 64 * R) ? 1 : 0;
+  return c;
+}
 
 // Sort A (nA keys in srt[]), exact prefix masses, the K / log c loop and the
-// systematic draws. scr: the W + key areas (W is overwritten).
-template <int NT, int R>
+// systematic draws. scr: the W + key areas (W is overwritten). The sort runs on
+// the first NSW waves (64 NSW R keys); the other waves of the workgroup only
+// pass its barriers.
+template <int NT, int NSW, int R>
 __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, int N, int M, int cnt_fin, const hyg_u192& massB,
                               unsigned char* scr, int* parents, Shared& sh, const ConstLds& cl, unsigned char* red,
                               float Usys, unsigned long long* ph, bool timed) {
+  static_assert(NSW <= NT / 64, "sorting waves");
   const int lane = lane_id();
+  const bool sorter = (NSW == NT / 64) || wave_id() < NSW;  // wave-uniform
   const int base = (int)(threadIdx.x >> 6) * 64 * R + lane * R;
   uint64_t e[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) e[r] = (base + r < nA) ? srt[base + r] : ~0ull;
-  int ib = 0;
-  Bitonic<NT, R, 2, 1>::run(e, (uint64_t*)scr, ib);
-  TPH(27);
-  // (every wave loaded its keys before the first cross-wave barrier)
-#pragma unroll
-  for (int r = 0; r < R; ++r) srt[base + r] = e[r];
   hyg_u192 f[R];
   hyg_u192 loc = hyg_u192_zero();
+  if (sorter) {
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const float m = hyg_expf(key_value(e[r]));
-    f[r] = hyg_fix149f((base + r < nA) ? m : 0.0f);
-    loc = hyg_u192_add(loc, f[r]);
+    for (int r = 0; r < R; ++r) e[r] = (base + r < nA) ? srt[base + r] : ~0ull;
+    int ib = 0;
+    Bitonic<64 * NSW, R, 2, 1>::run(e, (uint64_t*)scr, ib);
+    TPH(27);
+    // (every wave loaded its keys before the first cross-wave barrier)
+#pragma unroll
+    for (int r = 0; r < R; ++r) srt[base + r] = e[r];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float m = hyg_expf(key_value(e[r]));
+      f[r] = hyg_fix149f((base + r < nA) ? m : 0.0f);
+      loc = hyg_u192_add(loc, f[r]);
+    }
+  } else {
+    constexpr int nb = bitonic_lds_stages(64 * NSW * R, R);
+#pragma unroll
+    for (int i = 0; i < nb; ++i) lds_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      e[r] = ~0ull;
+      f[r] = hyg_u192_zero();
+    }
   }
   hyg_u192 massA;
   // red's last readers (the previous step's block max) are behind this step's
@@ -1027,10 +1071,12 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
   hyg_u192* pre = (hyg_u192*)scr;                           // inclusive prefix of sorted position p
   const hyg_u192 total = hyg_u192_add(massA, massB);         // every significant weight's mass
   hyg_u192 run = ex;
+  if (sorter) {
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    run = hyg_u192_add(run, f[r]);
-    if (base + r < nA) pre[base + r] = run;
+    for (int r = 0; r < R; ++r) {
+      run = hyg_u192_add(run, f[r]);
+      if (base + r < nA) pre[base + r] = run;
+    }
   }
   lds_barrier();
   TPH(28);
@@ -1116,30 +1162,12 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
   return sh.fast;
 }
 
-// hyg_fix149f for masses m < 2^-21 (image m 2^149 < 2^128): the two low words
-// of the same integer, the 24-bit significand shifted by E - 1 <= 105.
-__device__ __forceinline__ hyg_u128 fix149f_low128(float m) {
-  const uint32_t b = hyg_f32_bits(m);
-  const int E = (int)((b >> 23) & 0xff);
-  const uint64_t man = b & 0x7fffffu;
-  const uint64_t v = (E == 0) ? man : (man | 0x800000u);
-  const int sh = (E == 0) ? 0 : E - 1;
-  const int s0 = sh & 63;
-  const uint64_t lo = v << s0;
-  const uint64_t hi = (v >> 1) >> (63 - s0);  // v >> (64 - s0), 0 for s0 = 0
-  const bool zero = (b == 0) || (b >> 31);
-  hyg_u128 r;
-  r.lo = (zero || sh >= 64) ? 0 : lo;
-  r.hi = zero ? 0 : ((sh < 64) ? hi : lo);
-  return r;
-}
-
 // Top-set path of OptimalFiniteState; returns FAST_DONE (parents / Kk /
 // log_c written; log_c infinite -> the caller's unbiased fallback),
 // FAST_FALLBACK (W intact) or FAST_FALLBACK_REGEN (W overwritten). The
 // counts of the cutoff sets per wave (part_cnt) were published with the
 // candidate lists before the log-sum-exp reduction.
-template <int NT>
+template <int NT, int NSW>
 __device__ __forceinline__ int top_set_resample(const double* W, int N, double mx, double logS, const int* lst, int lb, int cw,
                                 unsigned char* scr, size_t scr_bytes, uint64_t* srt, size_t srt_bytes,
                                 const int* part_cnt, hyg_u192* part_tot, int* parents, Shared& sh,
@@ -1148,16 +1176,18 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
   constexpr int NW = NT / 64;
   const int wv = wave_id(), lane = lane_id();
   // ---- 1. the most inclusive cutoff whose set A fits the sort
-  // one LDS read per lane (lane w * kNCut + k holds wave w's count at cutoff
-  // k), the per-cutoff totals by xor shuffles (every lane l gets cutoff l % 8)
-  static_assert(kNCut == 8 && NW * kNCut <= 64, "cutoff counts: one per lane");
+  // one LDS read per lane per 8 waves (lane w * kNCut + k holds wave w's count
+  // at cutoff k, waves 8-15 in a second register), the per-cutoff totals by
+  // xor shuffles (every lane l gets cutoff l % 8)
+  static_assert(kNCut == 8 && NW * kNCut <= 128, "cutoff counts: one or two per lane");
   const int pc = (lane < NW * kNCut) ? part_cnt[lane] : 0;
-  int c = pc;
+  const int pc2 = (NW * kNCut > 64 && lane + 64 < NW * kNCut) ? part_cnt[lane + 64] : 0;
+  int c = pc + pc2;
   c += (int)xshfl32<8>((uint32_t)c);
   c += (int)xshfl32<16>((uint32_t)c);
   c += (int)xshfl32<32>((uint32_t)c);
-  const int np = (c <= 64 * NW) ? 64 * NW : 128 * NW;
-  const bool fits = lane < kNCut && c <= 64 * NW * rmax && (size_t)np * sizeof(hyg_u192) <= scr_bytes &&
+  const int np = (c <= 64 * NSW) ? 64 * NSW : 128 * NSW;
+  const bool fits = lane < kNCut && c <= 64 * NSW * rmax && (size_t)np * sizeof(hyg_u192) <= scr_bytes &&
                     (size_t)np * 8 <= srt_bytes;
   const uint64_t fm = wave_ballot(fits);
   const int nL = __builtin_amdgcn_readlane(c, kNCut - 1);
@@ -1168,15 +1198,17 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
   const bool hasB = nA < nL;         // list weights outside A (their masses enter the total)
   const double cutx = (ks == kNCut - 1) ? HYG_NINF : -cut_below_top(ks);
   int off = 0;
-  for (int w = 0; w < wv; ++w) off += __builtin_amdgcn_readlane(pc, w * kNCut + ks);
+  for (int w = 0; w < wv; ++w)
+    off += __builtin_amdgcn_readlane(w < 8 ? pc : pc2, (w & 7) * kNCut + ks);
   // ---- 2. gather A's keys; exact mass of the list weights outside A. From the
   // third cutoff on (X >= 20 nats below the top: every outside mass is below
   // e^-20 < 2^-28.8, its image m 2^149 below 2^120.2, and a lane sums at most
   // ceil(N / NT) <= 128 of them, below 2^127.2) a lane's images are formed and
   // summed as u128.
-  const bool narrow = ks >= 2 && (N + NT - 1) / NT <= 128;
+  const bool narrow = ks >= kNarrowCut && (N + NT - 1) / NT <= kNarrowPerLane;
   hyg_u192 mb = hyg_u192_zero(), mb2 = hyg_u192_zero();
   hyg_u128 nb = hyg_u128_zero(), nb2 = hyg_u128_zero();
+  constexpr int kLR = kLRof<NT>;
   for (int b = 0; b < cw; b += 64 * kLR) {  // kLR entries per lane, loads first (see the lse loop)
     int nn[kLR];
     float lw[kLR];
@@ -1204,7 +1236,7 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
 #pragma unroll
       for (int r = 0; r < kLR; ++r) {
         const float m = hyg_expf(lw[r]);
-        const hyg_u128 f = fix149f_low128(outA[r] ? m : 0.0f);
+        const hyg_u128 f = hyg_fix149f_low128(outA[r] ? m : 0.0f);
         if (r & 1) nb2 = hyg_u128_add(nb2, f); else nb = hyg_u128_add(nb, f);
       }
     } else if (hasB) {
@@ -1228,12 +1260,11 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
   }
   lds_barrier();
   hyg_u192 massB = hyg_u192_zero();
-  if (hasB)
-    for (int w = 0; w < NW; ++w) massB = hyg_u192_add(massB, part_tot[w]);
+  if (hasB) massB = sum_waves192<NW>(part_tot);
   TPH(26);
-  if (nA <= 64 * NW)
-    return top_set_finish<NT, 1>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
-  return top_set_finish<NT, 2>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
+  if (nA <= 64 * NSW)
+    return top_set_finish<NT, NSW, 1>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
+  return top_set_finish<NT, NSW, 2>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
 }
 #undef TPH
 
@@ -1277,8 +1308,11 @@ tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
 // M = 50, B = 25): K, M, B, the candidate count and the whole LDS layout are
 // then compile-time constants (LDS addresses fold into instruction offsets,
 // loops over slots get constant trip counts); KC = 0 reads them at run time.
+// Three waves per SIMD (<= 168 VGPRs) at 256, 384 and 768 threads: a CU holds
+// three, two or one chain(s) (the second argument is the minimum waves per
+// SIMD); 512 threads (the C5 kernel, one chain per CU by its LDS) may use 256.
 template <int NT, int KC = 0, int MC = 0, int BC = 0, bool PHS = false>  // PHS: phase-timer build
-__global__ void __launch_bounds__(NT, (NT <= 256 ? 3 : 1))
+__global__ void __launch_bounds__(NT, (NT == 512 ? 1 : 3))
 tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                   uint8_t* __restrict__ ws, int32_t* status_out, double* __restrict__ logz_out,
                   double* __restrict__ finalw_out, Lay lay_arg, unsigned long long* __restrict__ dbg_arg) {
@@ -1402,6 +1436,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       // code (hyg_fix100 is branch-free), so they interleave. fix100(exp(x))
       // is 0 for x < -70; padding lanes take x = -inf (mass 0, no cutoff).
       // Top-set steps also count the list per cutoff (per-lane counters).
+      constexpr int kLR = kLRof<NT>;
       hyg_u128 s0 = hyg_u128_zero(), s1 = hyg_u128_zero();
       int ccut[kNCut - 1];
 #pragma unroll
@@ -1476,7 +1511,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       PH(2);
       int fs = FAST_FALLBACK;
       if (topset)
-        fs = top_set_resample<NT>(W, N, mx, logS, lst, lst_base, lst_cnt, smem + lay.W, lay.bcnt - lay.W,
+        fs = top_set_resample<NT, kSortWaves<NT>>(W, N, mx, logS, lst, lst_base, lst_cnt, smem + lay.W, lay.bcnt - lay.W,
                                   (uint64_t*)(smem + lay.bcnt), lay.bcnt_bytes, part_cnt, part_tot, parents, sh, cl,
                                   red, M, cnt, Ucur, lay.topset_r, ph_acc, dbg != nullptr);
       PH(20);
@@ -1729,7 +1764,7 @@ __device__ __forceinline__ void backward_bits(uint64_t* rb, int B, int t, uint64
 }
 
 template <int NT, int KC = 0, int MC = 0, int BC = 0, bool PHS = false>  // KC > 0: one model shape (see tg_forward_kernel)
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT, (NT == 512 ? 1 : 3))
 tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                    const uint8_t* __restrict__ ws, const int32_t* status_in, int16_t* __restrict__ o_merged,
                    int16_t* __restrict__ o_control, int16_t* __restrict__ o_case, float* __restrict__ o_split,
@@ -2220,26 +2255,56 @@ void ev_record(int k, bool end, hipStream_t s) {
   (void)hipEventRecord(e, s);
   g_ev_used[k] = true;
 }
-// Threads per chain workgroup: HYG_THREADS (or HYG_THREADS_FWD / _BWD) if set;
-// otherwise 256, or 512 when the forward's LDS at 256 threads already forces one
-// workgroup per CU (K = 12, C5: 145 KB): the CU then holds one chain either
-// way, and twice the waves halve each thread's share of the N = M (2K + K^2)
-// candidates (C5: 5.67 M -> 6.52 M site-seeds/s).
-int threads_per_chain(bool backward, const hyg_tg_consts& c) {
+int device_cus() {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+// Threads per chain workgroup. HYG_THREADS (or HYG_THREADS_FWD / _BWD) if set.
+// Otherwise by what the launch's chains leave of the GPU. The pipeline-shape
+// kernels keep three waves per SIMD (<= 168 VGPRs, no spills) at every width,
+// so a CU holds k chains of 768 / k threads:
+//  - the forward's LDS at 256 threads already forces one workgroup per CU
+//    (K = 12, C5: 145 KB): 512, twice the waves on the CU's one chain;
+//  - at most one chain per CU (e.g. an 8-GPU rank of the C3 job, 73 chains):
+//    768 threads (kLowOccThreads), whose extra waves shorten each step of the
+//    sequential chain;
+//  - at most two per CU (an 8-GPU rank of C4, 291 chains): 384;
+//  - else 256, three chains per CU (C3 on one GPU: 582 chains).
+int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
   static int env[2] = {-1, -1};
+  static int lowocc = -1;
   const int k = backward ? 1 : 0;
   if (env[k] < 0) {
     const char* v = getenv(backward ? "HYG_THREADS_BWD" : "HYG_THREADS_FWD");
     if (!v) v = getenv("HYG_THREADS");
     const int x = v ? atoi(v) : 0;
-    env[k] = (x == 64 || x == 128 || x == 256 || x == 512) ? x : 0;
+    env[k] = (x == 64 || x == 128 || x == 256 || x == 384 || x == 512 || x == 768) ? x : 0;
+  }
+  if (lowocc < 0) {
+    const char* v = getenv("HYG_LOWOCC_THREADS");
+    const int x = v ? atoi(v) : 0;
+    lowocc = (x == 256 || x == 384 || x == 512 || x == 768) ? x : kLowOccThreads;
   }
   if (env[k]) return env[k];
   const int def = backward ? kDefaultThreadsBwd : kDefaultThreads;
   const size_t lds = make_layout(c.K, c.M, c.B, c.Nmax, def, false).total;
-  return (2 * lds > 160 * 1024) ? 512 : def;
+  if (2 * lds > 160 * 1024) return 512;
+  if (c.M > 64) return def;  // the wider kernels assume the pipeline's M <= 64 (one ancestor per lane)
+  const int cus = device_cus();
+  if (n_chains <= cus) return lowocc;
+  if (n_chains <= 2 * cus) return 384;
+  return def;
 }
 }  // namespace
+
+int tg_threads_per_chain(const hyg_tg_consts& c, int n_chains) { return threads_per_chain(false, c, n_chains); }
 
 void set_kernel_timing(bool on) { g_timing = on; }
 
@@ -2255,11 +2320,11 @@ int last_kernel_ms(float* out3) {
   return HYG_OK;
 }
 
-size_t forward_lds_bytes(const hyg_tg_consts& c) {
-  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(false, c), false).total;
+size_t forward_lds_bytes(const hyg_tg_consts& c, int n_chains) {
+  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(false, c, n_chains), false).total;
 }
-size_t backward_lds_bytes(const hyg_tg_consts& c) {
-  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(true, c), true).total;
+size_t backward_lds_bytes(const hyg_tg_consts& c, int n_chains) {
+  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(true, c, n_chains), true).total;
 }
 
 int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* meth_c, const uint16_t* tot_c,
@@ -2295,18 +2360,17 @@ static bool want_phases() {
   return on;
 }
 template <int NT>
-constexpr bool has_phases() { return NT == 256 || NT == 512; }
+constexpr bool has_phases() { return NT == 256 || NT == 512 || NT == 768; }
 template <int NT>
 FwdFn fwd_kernel(const hyg_tg_consts& c) {
   if constexpr (has_phases<NT>()) {
     if (want_phases()) {
-      if constexpr (NT == 256)
-        if (shape_specialised(c)) return &tg_forward_kernel<256, 6, 50, 25, true>;
+      if (shape_specialised(c)) return &tg_forward_kernel<NT, 6, 50, 25, true>;
       return &tg_forward_kernel<NT, 0, 0, 0, true>;
     }
   }
-  if constexpr (NT == 256)
-    if (shape_specialised(c)) return &tg_forward_kernel<256, 6, 50, 25>;
+  if constexpr (NT == 256 || NT == 384 || NT == 512 || NT == 768)
+    if (shape_specialised(c)) return &tg_forward_kernel<NT, 6, 50, 25>;
   if constexpr (NT == 512)
     if (shape_c5(c)) return &tg_forward_kernel<512, 12, 50, 25>;
   return &tg_forward_kernel<NT>;
@@ -2315,13 +2379,12 @@ template <int NT>
 BwdFn bwd_kernel(const hyg_tg_consts& c) {
   if constexpr (has_phases<NT>()) {
     if (want_phases()) {
-      if constexpr (NT == 256)
-        if (shape_specialised(c)) return &tg_backward_kernel<256, 6, 50, 25, true>;
+      if (shape_specialised(c)) return &tg_backward_kernel<NT, 6, 50, 25, true>;
       return &tg_backward_kernel<NT, 0, 0, 0, true>;
     }
   }
-  if constexpr (NT == 256)
-    if (shape_specialised(c)) return &tg_backward_kernel<256, 6, 50, 25>;
+  if constexpr (NT == 256 || NT == 384 || NT == 512 || NT == 768)
+    if (shape_specialised(c)) return &tg_backward_kernel<NT, 6, 50, 25>;
   if constexpr (NT == 512)
     if (shape_c5(c)) return &tg_backward_kernel<512, 12, 50, 25>;
   return &tg_backward_kernel<NT>;
@@ -2426,17 +2489,21 @@ int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* ch
   if (n_chains <= 0) return HYG_OK;
   hipStream_t s = (hipStream_t)stream;
   int rc;
-  switch (threads_per_chain(false, c)) {
+  switch (threads_per_chain(false, c, n_chains)) {
     case 64: rc = launch_forward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     case 128: rc = launch_forward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     case 256: rc = launch_forward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s); break;
+    case 384: rc = launch_forward_nt<384>(md, c, chains_dev, n_chains, E, ws, out, s); break;
+    case 768: rc = launch_forward_nt<768>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     default: rc = launch_forward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s); break;
   }
   if (rc != HYG_OK) return rc;
-  switch (threads_per_chain(true, c)) {
+  switch (threads_per_chain(true, c, n_chains)) {
     case 64: return launch_backward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s);
     case 128: return launch_backward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s);
     case 256: return launch_backward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s);
+    case 384: return launch_backward_nt<384>(md, c, chains_dev, n_chains, E, ws, out, s);
+    case 768: return launch_backward_nt<768>(md, c, chains_dev, n_chains, E, ws, out, s);
     default: return launch_backward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s);
   }
 }

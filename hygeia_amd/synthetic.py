@@ -43,8 +43,37 @@ def chromosome_sizes(total_sites: int, n_chrom: int = 22) -> np.ndarray:
     return sizes
 
 
-def _segments(rng, n: int, K: int, u: int, kappa: float, omega: float, start_regime=None):
+# single-group model of bin/simulate_data: per-regime omega
+SG_OMEGA = np.array([0.995, 0.975, 0.95, 0.925, 0.9, 0.9])
+
+
+def _segments_per_regime(rng, n: int, K: int, u: int, kappa: float, omega, start_regime=None):
+    """As _segments with a NegBin success probability per regime (the
+    single-group model's omega vector): the regime sequence first, then each
+    segment's length from its own regime's omega."""
+    omega = np.asarray(omega, np.float64)
+    mean_len = u + kappa * float(omega.min()) / (1 - float(omega.min()))
+    n_seg = int(n / max(mean_len, 1.0) * 1.3) + 16
+    first = rng.integers(0, K) if start_regime is None else start_regime
+    regs, lens, tot = [], [], 0
+    while tot < n:
+        steps = rng.integers(1, K, size=n_seg)  # uniform off-diagonal move
+        if regs:  # continue from the last regime
+            reg = (first + np.cumsum(steps)) % K
+        else:
+            reg = (first + np.concatenate([[0], np.cumsum(steps[1:])])) % K
+        ln = np.maximum(u + rng.negative_binomial(kappa, 1.0 - omega[reg]), 1)
+        regs.append(reg)
+        lens.append(ln)
+        tot += int(ln.sum())
+        first = int(reg[-1])
+    return np.repeat(np.concatenate(regs), np.concatenate(lens))[:n]
+
+
+def _segments(rng, n: int, K: int, u: int, kappa: float, omega, start_regime=None):
     """regime per site for n sites of a semi-Markov chain."""
+    if np.ndim(omega) > 0:
+        return _segments_per_regime(rng, n, K, u, kappa, omega, start_regime)
     mean_len = u + kappa * omega / (1 - omega)
     n_seg = int(n / max(mean_len, 1.0) * 1.3) + 16
     lens = u + rng.negative_binomial(kappa, 1.0 - omega, size=n_seg)
@@ -59,10 +88,12 @@ def _segments(rng, n: int, K: int, u: int, kappa: float, omega: float, start_reg
     return out
 
 
-def simulate(n_sites: int, n_ctrl: int, n_case: int, K: int = 6, u: int = 3, omega: float = 0.8,
+def simulate(n_sites: int, n_ctrl: int, n_case: int, K: int = 6, u: int = 3, omega=0.8,
              kappa: float = 2.0, coverage: float = 100.0, split_frac: float = 0.1, seed: int = DATA_SEED,
              mu=None, sigma=None):
-    """Returns dict with uint16 meth/total arrays [T][S] per group and the true regimes."""
+    """Returns dict with uint16 meth/total arrays [T][S] per group and the true
+    regimes. omega: the NegBin success probability of every regime, or one per
+    regime (SG_OMEGA, the single-group model)."""
     rng = np.random.default_rng(seed)
     if mu is None or sigma is None:
         mu, sigma = regime_params(K)
@@ -120,7 +151,7 @@ def segment_chains(chrom_sizes, segment_size: int = 100000, buffer_size: int = 5
     return chains
 
 
-def simulate_device(n_sites: int, n_ctrl: int, n_case: int, K: int = 6, u: int = 3, omega: float = 0.8,
+def simulate_device(n_sites: int, n_ctrl: int, n_case: int, K: int = 6, u: int = 3, omega=0.8,
                     kappa: float = 2.0, coverage: float = 100.0, split_frac: float = 0.1, seed: int = DATA_SEED,
                     device=None):
     """simulate() with the per-sample draws (Beta levels, Poisson coverage,

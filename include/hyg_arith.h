@@ -369,6 +369,26 @@ HYG_HD hyg_u192 hyg_fix149f(float m) {
   return r;
 }
 
+/* hyg_fix149f for masses m < 2^-21 (image m 2^149 < 2^128): the two low words
+ * of the same integer, the 24-bit significand shifted by E - 1 <= 105. Used by
+ * the top-set resampling path for masses it has proved small (tg_kernels.hip);
+ * tests/test_arith_carry.py checks it against hyg_fix149f. */
+HYG_HD hyg_u128 hyg_fix149f_low128(float m) {
+  const uint32_t b = hyg_f32_bits(m);
+  const int E = (int)((b >> 23) & 0xff);
+  const uint64_t man = b & 0x7fffffu;
+  const uint64_t v = (E == 0) ? man : (man | 0x800000u);
+  const int sh = (E == 0) ? 0 : E - 1;
+  const int s0 = sh & 63;
+  const uint64_t lo = v << s0;
+  const uint64_t hi = (v >> 1) >> (63 - s0); /* v >> (64 - s0), 0 for s0 = 0 */
+  const int zero = (b == 0) || (b >> 31);
+  hyg_u128 r;
+  r.lo = (zero || sh >= 64) ? 0 : lo;
+  r.hi = zero ? 0 : ((sh < 64) ? hi : lo);
+  return r;
+}
+
 /* value * 2^-149 as a double: top 53 bits (truncated), exactly scaled. */
 HYG_HD double hyg_u192_to_f64(hyg_u192 a) {
   int p;

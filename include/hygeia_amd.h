@@ -26,6 +26,15 @@
  * hipStream_t (NULL = the default stream) and take DEVICE pointers; functions
  * named *_host take host pointers and synchronise. There is no CPU fallback:
  * without a HIP device every compute entry point returns HYG_EDEVICE.
+ *
+ * Threading: a model handle (hyg_tg_model / hyg_sg_model) is read-only after
+ * creation except for its per-stream pinned staging buffers, which are
+ * mutex-guarded; several host threads may launch with one model, each on its
+ * own stream, without waiting for each other's kernels. hyg_set_kernel_timing /
+ * hyg_tg_last_kernel_ms are a process-wide diagnostic and are not thread-safe.
+ * The single-group chain launches need two workgroups per chain resident at
+ * once; they stay correct on a shared GPU (a chain's pair then waits for a
+ * free CU) but are sized for a GPU they have to themselves.
  */
 #ifndef HYGEIA_AMD_H
 #define HYGEIA_AMD_H
@@ -96,6 +105,14 @@ void hyg_tg_model_destroy(hyg_tg_model* model);
 /* Derived sizes: I = 2K + K^2 proposal slots, N_max = M * I particles
  * (run_inference_two_groups.py:263,285). */
 int32_t hyg_tg_num_particles(const hyg_tg_model* model);
+
+/* Threads per chain workgroup of the forward kernel for a launch of n_chains
+ * chains on the current device: 256 (three chains per CU), 512 (up to 1.25
+ * chains per CU) or the low-occupancy width (at most one chain per CU), whose
+ * extra waves shorten each step of the sequential chain. Diagnostic: the
+ * launch functions choose it themselves. No reference counterpart (the
+ * reference runs one chain per CPU process, modules/two_group/4_infer.nf:28). */
+int32_t hyg_tg_threads_per_chain(const hyg_tg_model* model, int32_t n_chains);
 
 /* Per-site emission table E[t][g*K + r] = log g_t for group g (0 control,
  * 1 case) and regime r: sum over samples of BetaBinomial(meth | total,

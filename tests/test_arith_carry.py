@@ -80,3 +80,62 @@ def test_carry_chain_forms_match_exact_integers(tmp_path):
             assert _join(f[11:14]) == abs(x - y)
             n192 += 1
     assert n128 == 4000 and n192 == 4000
+
+
+PROG_LOW128 = r"""
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include "hyg_arith.h"
+static uint64_t st = 0x2545F4914F6CDD1Dull;
+static uint64_t nx() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; }
+static void show(uint32_t b) {
+  float m;
+  std::memcpy(&m, &b, 4);
+  const hyg_u192 w = hyg_fix149f(m);
+  const hyg_u128 n = hyg_fix149f_low128(m);
+  printf("%08x %016llx %016llx %016llx %016llx %016llx\n", b, (unsigned long long)w.w0, (unsigned long long)w.w1,
+         (unsigned long long)w.w2, (unsigned long long)n.lo, (unsigned long long)n.hi);
+}
+int main() {
+  // every exponent below 2^-21 (E = 0 subnormals .. 105), incl. the word
+  // boundary sh = E - 1 = 63 / 64, with edge significands
+  for (uint32_t E = 0; E <= 105; ++E) {
+    const uint32_t mans[4] = {0u, 1u, 0x7fffffu, (uint32_t)(nx() & 0x7fffffu)};
+    for (int i = 0; i < 4; ++i) show((E << 23) | mans[i]);
+  }
+  for (int i = 0; i < 3000; ++i) show((uint32_t)(nx() % (106u << 23)));
+  show(0x80000000u);  // -0 and negative masses image to 0
+  show(0x80000001u);
+  return 0;
+}
+"""
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_fix149f_low128_equals_fix149f_below_2_pow_minus_21(tmp_path):
+    """the narrow u128 image of the top-set outside masses equals the
+    low two words of hyg_fix149f (whose top word is 0) for every f32 m < 2^-21,
+    subnormals and the sh = 63 / 64 word boundary included."""
+    src = tmp_path / "low128.hip"
+    exe = tmp_path / "low128"
+    src.write_text(PROG_LOW128)
+    subprocess.run([HIPCC, "-O2", "-std=c++17", "-I", os.path.join(REPO, "include"), "-o", str(exe), str(src)],
+                   check=True, capture_output=True, timeout=300)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True, timeout=60).stdout.split("\n")
+    import struct
+    n = 0
+    for line in out:
+        f = line.split()
+        if not f:
+            continue
+        b = int(f[0], 16)
+        w0, w1, w2, lo, hi = (int(x, 16) for x in f[1:])
+        m = struct.unpack("<f", struct.pack("<I", b))[0]
+        assert m < 2.0 ** -21
+        exact = 0 if (b >> 31) else int(round(m * 2.0 ** 149)) if m > 0 else 0
+        assert (w0 | (w1 << 64) | (w2 << 128)) == exact
+        assert w2 == 0
+        assert (lo, hi) == (w0, w1)
+        n += 1
+    assert n == 106 * 4 + 3000 + 2

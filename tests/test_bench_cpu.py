@@ -1,5 +1,5 @@
-"""bench.py's host-side logic on CPU: the chain lists of the c3 (weak) and c4
-(strong, LPT-sharded) jobs, the host-core accounting of the CPU baseline, and
+"""bench.py's host-side logic on CPU: the chain lists of the c3 and c4 jobs
+(fixed jobs, LPT-sharded over the ranks), the host-core accounting of the CPU baseline, and
 the c4 job end to end over torch.distributed ("gloo", world size 2) with the
 oracle standing in for the GPU chains (test infrastructure)."""
 import argparse
@@ -19,18 +19,20 @@ def _args(job, **kw):
     return a
 
 
-def test_c3_weak_chains_per_rank():
+def test_c3_strong_chains_cover_the_fixed_job_once():
+    """at N > 1 GPUs the c3 job is the metric's fixed 2-seed job
+    (582 chains at 28M sites), split over the ranks, not 2 seeds per rank."""
     segs = synthetic.segment_chains(synthetic.chromosome_sizes(1_000_000))
-    for world in (1, 2, 4):
-        seen = set()
+    job = {((ci << 32) | b, sd) for sd in range(2) for (ci, b, *_r) in segs}
+    for world in (1, 2, 4, 8):
+        got, units_total = [], 0
         for rank in range(world):
             chains, n_out, units, picked = bench.build_chains(_args("c3"), segs, rank, world)
-            seeds = {c[2] for c in chains}
-            assert seeds == {2 * rank, 2 * rank + 1}  # every rank its own seeds
-            assert units == 2 * sum(s[5] for s in segs)
+            got += [(c[3], c[2]) for c in chains]
+            units_total += units
             assert n_out == sum(c[1] for c in chains)
-            assert not (seen & seeds)
-            seen |= seeds
+        assert sorted(got) == sorted(job) and len(got) == len(job)
+        assert units_total == 2 * sum(s[5] for s in segs)
 
 
 def test_c4_strong_chains_cover_the_job_once():

@@ -11,7 +11,11 @@ the CPU oracle, every output array compared):
   the int16 duration outputs (run_inference_two_groups.py:292-314);
 - C2 (configs[1]): one single-group chain of 200 000 sites at the pipeline
   settings (4 samples, K = 6, N_max = 250, epsilon = 0.01), long enough for the
-  log-weights to reach the large-magnitude regime noted in DESIGN.md 1.
+  log-weights to reach the large-magnitude regime noted in DESIGN.md 1;
+- C1 (configs[0]): the whole chr21-sized single-group chain (454 914 sites of
+  the 28M-site genome), 2 samples, K = 6, N_max = 250,
+  epsilon = 0.01, 1 seed, data from the single-group model (per-regime omega),
+  as estimate_parameters_and_regimes:303-322 runs it per chromosome.
 
 The oracle chains take about a minute each on one core; they run in threads
 (ctypes releases the GIL) started when the module is first used, overlapping
@@ -73,10 +77,17 @@ def long_refs(oracle):
         E = sgb.emission(psg, sgd["meth_control"], sgd["tot_control"])
         return sgb.chain(psg, E, seed=3, chain_id=5)
 
-    ex = cf.ThreadPoolExecutor(max_workers=3)
-    futs = {"synthetic": ex.submit(tg, "synthetic"), "one_regime": ex.submit(tg, "one_regime"),
-            "sg": ex.submit(sgchain)}
-    yield data, futs, (sgd, psg)
+    c1d = syn.simulate(int(syn.chromosome_sizes(28_000_000)[20]), 2, 1, K=6, seed=2121, coverage=100.0,
+                       omega=syn.SG_OMEGA)
+
+    def c1chain():
+        E = sgb.emission(psg, c1d["meth_control"], c1d["tot_control"])
+        return sgb.chain(psg, E, seed=1, chain_id=20)
+
+    ex = cf.ThreadPoolExecutor(max_workers=4)
+    futs = {"c1": ex.submit(c1chain), "synthetic": ex.submit(tg, "synthetic"),
+            "one_regime": ex.submit(tg, "one_regime"), "sg": ex.submit(sgchain)}
+    yield data, futs, (sgd, psg, c1d)
     ex.shutdown(wait=True)
 
 
@@ -153,26 +164,44 @@ def test_c3_full_length_chain(oracle, long_refs, name):
         assert dur.min() < 0  # the int16 duration output wrapped (sojourn > 32767 sites)
 
 
-@pytest.mark.timeout(600)
-def test_c2_single_group_200k_chain(long_refs):
+def _sg_host_chain(psg, meth, tot, seed, chain_id):
     from hygeia_amd import _lib
 
-    _, futs, (sgd, psg) = long_refs
     L = _lib.load()
     p = _lib.SgParams.from_buffer_copy(bytes(psg))
     h = C.c_void_p()
-    meth = np.ascontiguousarray(sgd["meth_control"], np.uint16)
-    tot = np.ascontiguousarray(sgd["tot_control"], np.uint16)
+    meth = np.ascontiguousarray(meth, np.uint16)
+    tot = np.ascontiguousarray(tot, np.uint16)
     T, S = tot.shape
     _lib.check(L.hyg_sg_model_create(C.byref(p), int(tot.max()), T + 10, C.byref(h)))
     try:
         out = np.full((T, 6), np.nan)
-        rc = L.hyg_sg_run_chain_host(h, meth.ctypes.data_as(C.c_void_p), tot.ctypes.data_as(C.c_void_p), S, T, 3, 5,
-                                     out.ctypes.data_as(C.c_void_p))
+        rc = L.hyg_sg_run_chain_host(h, meth.ctypes.data_as(C.c_void_p), tot.ctypes.data_as(C.c_void_p), S, T, seed,
+                                     chain_id, out.ctypes.data_as(C.c_void_p))
         assert rc == 0, L.hyg_last_error()
     finally:
         L.hyg_sg_model_destroy(h)
+    return out
+
+
+@pytest.mark.timeout(600)
+def test_c2_single_group_200k_chain(long_refs):
+    _, futs, (sgd, psg, _) = long_refs
+    out = _sg_host_chain(psg, sgd["meth_control"], sgd["tot_control"], 3, 5)
     ref = futs["sg"].result()
+    assert ref["status"] == 0
+    bad = np.argwhere(out != ref["regime_probs"])
+    assert bad.size == 0, (len(bad), bad[:5])
+    np.testing.assert_allclose(out.sum(1), 1.0, atol=1e-8)
+
+
+@pytest.mark.timeout(600)
+def test_c1_single_group_chr21_chain(long_refs):
+    """C1 in full: the chr21-sized chain (454 914 sites), S = 2, bit-exact."""
+    _, futs, (_, psg, c1d) = long_refs
+    assert c1d["tot_control"].shape == (454914, 2)
+    out = _sg_host_chain(psg, c1d["meth_control"], c1d["tot_control"], 1, 20)
+    ref = futs["c1"].result()
     assert ref["status"] == 0
     bad = np.argwhere(out != ref["regime_probs"])
     assert bad.size == 0, (len(bad), bad[:5])

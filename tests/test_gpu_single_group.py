@@ -225,6 +225,14 @@ def test_invalid_inputs(lib, sg):
         tot = np.array([[3], [1]], np.uint16)  # y > n at site 1: all weights -inf
         rc, _ = m.chain_host(meth, tot, 0, 0)
         assert rc == _lib.HYG_ENUMERIC
+        # y > n at site 0: no finite initial weight. The SMC workgroup must
+        # publish the abort at t = 0 (it used to return silently and
+        # leave the smoothing workgroup polling for ~25 s, then HYG_EDEVICE)
+        import time
+        t0 = time.perf_counter()
+        rc, _ = m.chain_host(np.array([[4], [1]], np.uint16), np.array([[3], [2]], np.uint16), 0, 0)
+        assert rc == _lib.HYG_ENUMERIC
+        assert time.perf_counter() - t0 < 5.0
         long = np.zeros((101, 1), np.uint16)  # longer than max_duration
         rc, _ = m.chain_host(long, long, 0, 0)
         assert rc == _lib.HYG_EINVAL

@@ -5,9 +5,10 @@ Each configuration runs many seeds as chains of ONE batched launch
 (1) bit for bit with the CPU oracle, chain by chain, and
 (2) with the exact enumeration of the model (tests/tg_exact_model.py): in the
     keep-all regime the GPU's log Z equals the exact log marginal likelihood
-    given the phantom regime to 1e-12; with M = 2-3 (optimal finite-state
-    resampling active) the seed average of Z_hat / Z stays 1 within its
-    standard error.
+    given the phantom regime to 1e-12 and the GPU's backward draws pass the
+    chi-square tests against the exact smoother; with M = 2-3 (optimal
+    finite-state resampling active) the seed average of Z_hat / Z stays 1
+    within its standard error. Cases at u = 2, the pipeline's u = 3, and u = 4.
 """
 import math
 import os
@@ -21,7 +22,8 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from test_tg_exact import KEEP_ALL_CASES, KEEP_ALL_M, RESAMPLING_CASES, _problem  # noqa: E402
+from test_tg_exact import (BACKWARD_CASES, KEEP_ALL_CASES, KEEP_ALL_M, RESAMPLING_CASES, _problem,  # noqa: E402
+                           check_draws_follow_exact_smoother)
 from tg_exact_model import phantom_regime  # noqa: E402
 
 
@@ -66,10 +68,10 @@ def _check_chain_bits(oracle, p, E, dc, i, seed, cid, T):
     np.testing.assert_array_equal(dc.final_w[i].cpu().numpy(), ref["final_log_weights"])
 
 
-@pytest.mark.parametrize("K,T,dseed", KEEP_ALL_CASES)
-def test_keep_all_gpu_vs_oracle_and_exact(oracle, K, T, dseed):
+@pytest.mark.parametrize("K,T,dseed,u", KEEP_ALL_CASES)
+def test_keep_all_gpu_vs_oracle_and_exact(oracle, K, T, dseed, u):
     B = 8
-    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=KEEP_ALL_M, B=B)
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=KEEP_ALL_M, B=B, u=u)
     seeds = list(range(24))
     cid = 40
     dc = _run_seeds(p, E, K, KEEP_ALL_M, B, seeds, cid)
@@ -84,9 +86,9 @@ def test_keep_all_gpu_vs_oracle_and_exact(oracle, K, T, dseed):
     assert len(exact) >= 2
 
 
-@pytest.mark.parametrize("K,T,M,dseed", RESAMPLING_CASES)
-def test_resampling_gpu_vs_oracle_and_unbiased_z(oracle, K, T, M, dseed):
-    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2)
+@pytest.mark.parametrize("K,T,M,dseed,u", RESAMPLING_CASES)
+def test_resampling_gpu_vs_oracle_and_unbiased_z(oracle, K, T, M, dseed, u):
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2, u=u)
     seeds = list(range(8192))
     cid = 3
     dc = _run_seeds(p, E, K, M, 2, seeds, cid)
@@ -103,3 +105,19 @@ def test_resampling_gpu_vs_oracle_and_unbiased_z(oracle, K, T, M, dseed):
     r = np.array(ratios)
     se = r.std() / math.sqrt(len(r))
     assert abs(r.mean() - 1.0) < 4 * se + 1e-3, (r.mean(), se)
+
+
+@pytest.mark.parametrize("K,T,dseed,u", BACKWARD_CASES)
+def test_backward_gpu_draws_follow_exact_smoother(oracle, K, T, dseed, u):
+    M, B, nseeds, cid = KEEP_ALL_M, 60, 300, 7
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=B, cov=2, u=u)
+    seeds = list(range(nseeds))
+    dc = _run_seeds(p, E, K, M, B, seeds, cid)
+    for i in range(0, nseeds, 37):
+        _check_chain_bits(oracle, p, E, dc, i, seeds[i], cid, T)
+    mg, ct, cs = dc.merged.cpu().numpy(), dc.control.cpu().numpy(), dc.case.cpu().numpy()
+
+    def paths_of(i, seed):
+        return mg[i * T:(i + 1) * T], ct[i * T:(i + 1) * T], cs[i * T:(i + 1) * T]
+
+    check_draws_follow_exact_smoother(oracle, ex, E_ex, K, T, u, B, seeds, cid, paths_of)

@@ -5,7 +5,14 @@ runs one R process per (sample group, chromosome); one "step" = emission table
 + SMC / optimal resampling / online marginal smoothing of every chain, counts
 resident in HBM. Prints one JSON line in bench.py's format (units = CpG sites).
 
-    python tools/bench_sg.py [--sites N] [--steps K] [--warmup W] [--per-sample]
+    python tools/bench_sg.py [--config c1|c2] [--sites N] [--steps K] [--warmup W] [--per-sample]
+
+--config c1 is BASELINE.json configs[0]: the chr21-sized chain of the same
+genome (454 914 sites), 2 samples, K = 6, 1 seed; its CPU baseline times the
+oracle/ restatement on ALL of C1 (one thread: the reference runs one R process
+per chromosome), as BASELINE.md 3 asks. Both configs draw the data from the
+single-group model of bin/simulate_data (per-regime omega) at the
+reference's default coverage lambda = 100.
 
 --estimate-parameters runs the two-group pipeline's actual stage 2
 (2_estimate_parameters_and_regimes.nf: --estimate_regime_probabilities
@@ -83,10 +90,11 @@ def cpu_baseline(meth, tot, chains, params, seconds, threads, pe=False):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sites", type=int, default=28_000_000)
-    ap.add_argument("--samples", type=int, default=4)
+    ap.add_argument("--config", choices=("c1", "c2"), default="c2")
+    ap.add_argument("--sites", type=int, default=None, help="default: 28M (c2), the chr21 share of 28M (c1)")
+    ap.add_argument("--samples", type=int, default=None, help="default: 4 (c2), 2 (c1)")
     ap.add_argument("--K", type=int, default=6)
-    ap.add_argument("--coverage", type=float, default=30.0)
+    ap.add_argument("--coverage", type=float, default=100.0, help="Poisson lambda (SURVEY.md 8d default 100)")
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=0)
     ap.add_argument("--psi-capacity", type=int, default=0)
@@ -101,6 +109,13 @@ def main():
 
     from hygeia_amd import _lib, synthetic
 
+    c1 = args.config == "c1"
+    chr21 = int(synthetic.chromosome_sizes(28_000_000)[20])
+    if args.sites is None:
+        args.sites = chr21 if c1 else 28_000_000
+    if args.samples is None:
+        args.samples = 2 if c1 else 4
+
     # the chain kernel runs for minutes: a heartbeat keeps the run visibly alive
     t_start = time.perf_counter()
 
@@ -114,10 +129,11 @@ def main():
     dev = torch.device("cuda", 0)
     L = _lib.load()
     K, S = args.K, args.samples
-    d = synthetic.simulate_device(args.sites, S, 1, K=K, coverage=args.coverage, device=dev)
+    d = synthetic.simulate_device(args.sites, S, 1, K=K, coverage=args.coverage, omega=synthetic.SG_OMEGA,
+                                  device=dev)
     meth, tot = d["meth_control"], d["tot_control"]
     del d["meth_case"], d["tot_case"]
-    sizes = synthetic.chromosome_sizes(args.sites)
+    sizes = np.array([args.sites]) if c1 else synthetic.chromosome_sizes(args.sites)
     begins = np.concatenate([[0], np.cumsum(sizes)[:-1]])
     n_rows = args.sites  # rows of the emission / output tables
     if args.per_sample:  # sample-major [S][T][1]: sample s's chain rows start at s * T
@@ -128,7 +144,7 @@ def main():
               for i, (b, n) in enumerate(zip(begins, sizes))]
         S = 1
     else:
-        cl = [(int(b), int(n), i) for i, (b, n) in enumerate(zip(begins, sizes))]
+        cl = [(int(b), int(n), 20 if c1 else i) for i, (b, n) in enumerate(zip(begins, sizes))]
     chains = sorted(cl, key=lambda c: -c[1])
     arr = (_lib.SgChain * len(chains))()
     for i, (b, n, ci) in enumerate(chains):
@@ -210,7 +226,9 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": (f"C2 single_group {args.sites} CpG x {args.samples} samples, one chain per "
                                 f"(sample, chromosome) = {len(chains)} chains of 1 sample" if args.per_sample else
+                                f"C1 single_group chr21 {args.sites} CpG, one chain, {S} samples" if c1 else
                                 f"C2 single_group {args.sites} CpG, 22 chromosome chains, {S} samples jointly")
+                               + ", single-group model data (per-regime omega)"
                                + f", K={K}, N_max=250, epsilon=0.01, 1 seed, coverage {args.coverage}"
                                + (", online parameter estimation (ADAM, update every 200 steps)"
                                   if pe is not None else ""),
@@ -222,7 +240,22 @@ def main():
                      "kernel_ms": {"sg_emission_kernel": float(kavg[0]), "sg_chain_kernel": float(kavg[1])},
                      "us_per_step_longest_chain": float(kavg[1] * 1000.0 / max(sizes))},
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and c1:
+        import bench
+        from oracle import sg_binding as sb
+
+        # C1 in full on the CPU: the restatement over the whole chain, one thread
+        mh, th = meth.cpu().numpy().view(np.uint16), tot.cpu().numpy().view(np.uint16)
+        pc = sb.SgParams.from_buffer_copy(bytes(p))
+        t0 = time.perf_counter()
+        out = sb.chain(pc, sb.emission(pc, mh, th), 1, 20)
+        dt_cpu = time.perf_counter() - t0
+        assert out["status"] == 0
+        line["cpu_baseline"] = {"value": args.sites / dt_cpu, "unit": "CpG-sites/s", "cores": 1, "kind": "port",
+                                "sample": f"the whole C1 chain ({args.sites} sites) in full: oracle/sg_oracle.c "
+                                          f"emission + SMC + online smoothing, {dt_cpu:.1f} s",
+                                "host": bench.host_cpus()}
+    elif not args.no_cpu_baseline:
         import bench
 
         host = bench.host_cpus()
