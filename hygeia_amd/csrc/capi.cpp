@@ -299,6 +299,11 @@ int32_t hyg_tg_threads_per_chain(const hyg_tg_model* m, int32_t n_chains) {
   return m ? hyg::tg_threads_per_chain(m->c, n_chains) : 0;
 }
 
+int hyg_tg_force_threads(int32_t forward, int32_t backward) {
+  const int rc = hyg::tg_force_threads(forward, backward);
+  return rc == HYG_OK ? rc : fail(rc, "unsupported workgroup size");
+}
+
 int hyg_tg_emission(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_t* tot_c, int32_t s_c,
                     const uint16_t* meth_k, const uint16_t* tot_k, int32_t s_k, int64_t n_sites, double* E,
                     void* stream) {

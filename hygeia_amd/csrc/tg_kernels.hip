@@ -1269,45 +1269,60 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
 #undef TPH
 
 // --------------------------------------------------------------- kernels
-__global__ void __launch_bounds__(256)
+// One thread per site of a 256-site tile; the tile's rows [256][2K] f64 are
+// assembled in LDS and written out as whole 16-byte pieces by consecutive
+// lanes (a thread writing its own 96-byte row in 8-byte stores left partial
+// lines: 1.36x the algorithmic write bytes at K = 6).
+constexpr int kETile = 256;
+__global__ void __launch_bounds__(kETile)
 tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg, const double* __restrict__ cst,
                    int L, int K, const uint16_t* __restrict__ meth_c, const uint16_t* __restrict__ tot_c, int s_c,
                    const uint16_t* __restrict__ meth_k, const uint16_t* __restrict__ tot_k, int s_k, int64_t T,
                    double* __restrict__ E) {
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (int64_t)gridDim.x * blockDim.x) {
-    for (int g = 0; g < 2; ++g) {
-      const int S = g ? s_k : s_c;
-      const uint16_t* my = g ? meth_k + t * s_k : meth_c + t * s_c;
-      const uint16_t* nt = g ? tot_k + t * s_k : tot_c + t * s_c;
-      double e[HYG_KMAX];
-      for (int r = 0; r < K; ++r) e[r] = 0.0;
-      for (int s = 0; s < S; ++s) {
-        const int n = nt[s], y = my[s];
-        if (n == 0) continue;
-        if (y > n || n >= L) {  // invalid input: poison the row
-          for (int r = 0; r < K; ++r) e[r] = HYG_NAN;
-          break;
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* tile = (double*)smem;  // [kETile][2K]
+  const int K2 = 2 * K;
+  for (int64_t t0 = (int64_t)blockIdx.x * kETile; t0 < T; t0 += (int64_t)gridDim.x * kETile) {
+    const int64_t t = t0 + threadIdx.x;
+    if (t < T) {
+      for (int g = 0; g < 2; ++g) {
+        const int S = g ? s_k : s_c;
+        const uint16_t* my = g ? meth_k + t * s_k : meth_c + t * s_c;
+        const uint16_t* nt = g ? tot_k + t * s_k : tot_c + t * s_c;
+        double e[HYG_KMAX];
+        for (int r = 0; r < K; ++r) e[r] = 0.0;
+        for (int s = 0; s < S; ++s) {
+          const int n = nt[s], y = my[s];
+          if (n == 0) continue;
+          if (y > n || n >= L) {  // invalid input: poison the row
+            for (int r = 0; r < K; ++r) e[r] = HYG_NAN;
+            break;
+          }
+          double base = lf[n] - lf[y];
+          base = base - lf[n - y];
+          for (int r = 0; r < K; ++r) {
+            double term = base + lg[(size_t)(r * 3 + 0) * L + y];
+            term = term + lg[(size_t)(r * 3 + 1) * L + (n - y)];
+            term = term - lg[(size_t)(r * 3 + 2) * L + n];
+            term = term + cst[r];
+            e[r] = e[r] + term;
+          }
         }
-        double base = lf[n] - lf[y];
-        base = base - lf[n - y];
-        for (int r = 0; r < K; ++r) {
-          double term = base + lg[(size_t)(r * 3 + 0) * L + y];
-          term = term + lg[(size_t)(r * 3 + 1) * L + (n - y)];
-          term = term - lg[(size_t)(r * 3 + 2) * L + n];
-          term = term + cst[r];
-          e[r] = e[r] + term;
-        }
+        for (int r = 0; r < K; ++r) tile[threadIdx.x * K2 + g * K + r] = e[r];
       }
-      for (int r = 0; r < K; ++r) E[t * 2 * K + g * K + r] = e[r];
     }
+    __syncthreads();
+    // the tile's rows are contiguous in E: 16-byte pieces, consecutive lanes
+    const int64_t rows = (T - t0) < kETile ? (T - t0) : kETile;
+    const int n = (int)rows * K2;  // doubles; E rows start 16-byte aligned when K2 is even
+    double* dst = E + t0 * K2;
+    for (int i = 2 * threadIdx.x; i + 1 < n; i += 2 * kETile)
+      *(double2*)(dst + i) = make_double2(tile[i], tile[i + 1]);
+    if ((n & 1) && threadIdx.x == 0) dst[n - 1] = tile[n - 1];
+    __syncthreads();
   }
 }
 
-// 3 workgroups per CU at NT = 256 (<= 168 VGPRs): all C3 chains resident at once.
-// KC/MC/BC > 0: an instantiation for one model shape (the pipeline's K = 6,
-// M = 50, B = 25): K, M, B, the candidate count and the whole LDS layout are
-// then compile-time constants (LDS addresses fold into instruction offsets,
-// loops over slots get constant trip counts); KC = 0 reads them at run time.
 // Three waves per SIMD (<= 168 VGPRs) at 256, 384 and 768 threads: a CU holds
 // three, two or one chain(s) (the second argument is the minimum waves per
 // SIMD); 512 threads (the C5 kernel, one chain per CU by its LDS) may use 256.
@@ -2277,7 +2292,10 @@ int device_cus() {
 //    sequential chain;
 //  - at most two per CU (an 8-GPU rank of C4, 291 chains): 384;
 //  - else 256, three chains per CU (C3 on one GPU: 582 chains).
+int g_force_threads[2] = {0, 0};  // hyg_tg_force_threads (tests): forward, backward; 0 = automatic
+bool valid_width(int x) { return x == 64 || x == 128 || x == 256 || x == 384 || x == 512 || x == 768; }
 int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
+  if (g_force_threads[backward ? 1 : 0]) return g_force_threads[backward ? 1 : 0];
   static int env[2] = {-1, -1};
   static int lowocc = -1;
   const int k = backward ? 1 : 0;
@@ -2285,7 +2303,7 @@ int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
     const char* v = getenv(backward ? "HYG_THREADS_BWD" : "HYG_THREADS_FWD");
     if (!v) v = getenv("HYG_THREADS");
     const int x = v ? atoi(v) : 0;
-    env[k] = (x == 64 || x == 128 || x == 256 || x == 384 || x == 512 || x == 768) ? x : 0;
+    env[k] = valid_width(x) ? x : 0;
   }
   if (lowocc < 0) {
     const char* v = getenv("HYG_LOWOCC_THREADS");
@@ -2305,6 +2323,12 @@ int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
 }  // namespace
 
 int tg_threads_per_chain(const hyg_tg_consts& c, int n_chains) { return threads_per_chain(false, c, n_chains); }
+int tg_force_threads(int fwd, int bwd) {
+  if ((fwd && !valid_width(fwd)) || (bwd && !valid_width(bwd))) return HYG_EINVAL;
+  g_force_threads[0] = fwd;
+  g_force_threads[1] = bwd;
+  return HYG_OK;
+}
 
 void set_kernel_timing(bool on) { g_timing = on; }
 
@@ -2331,11 +2355,12 @@ int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* 
                     int s_c, const uint16_t* meth_k, const uint16_t* tot_k, int s_k, int64_t n_sites, double* E,
                     void* stream) {
   if (n_sites <= 0) return HYG_OK;
-  int64_t blocks = (n_sites + 255) / 256;
+  int64_t blocks = (n_sites + kETile - 1) / kETile;
   if (blocks > 256 * 16) blocks = 256 * 16;
   ev_record(0, false, (hipStream_t)stream);
-  hipLaunchKernelGGL(tg_emission_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, md.lf, md.lg,
-                     md.cst, md.nmax_reads + 1, c.K, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E);
+  const size_t lds = sizeof(double) * kETile * 2 * c.K;
+  hipLaunchKernelGGL(tg_emission_kernel, dim3((unsigned)blocks), dim3(kETile), lds, (hipStream_t)stream, md.lf,
+                     md.lg, md.cst, md.nmax_reads + 1, c.K, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E);
   ev_record(0, true, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }

@@ -114,6 +114,12 @@ int32_t hyg_tg_num_particles(const hyg_tg_model* model);
  * reference runs one chain per CPU process, modules/two_group/4_infer.nf:28). */
 int32_t hyg_tg_threads_per_chain(const hyg_tg_model* model, int32_t n_chains);
 
+/* Test / tuning override of the chain workgroup sizes for every later launch
+ * in the process: forward and backward threads (64, 128, 256, 384, 512 or 768;
+ * 0 = the automatic choice above). Not thread-safe. The results do not depend
+ * on it: every width computes the same bits. */
+int hyg_tg_force_threads(int32_t forward, int32_t backward);
+
 /* Per-site emission table E[t][g*K + r] = log g_t for group g (0 control,
  * 1 case) and regime r: sum over samples of BetaBinomial(meth | total,
  * alpha_r, beta_r) (case_control_regime_model.py:197-231). Counts are

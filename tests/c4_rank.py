@@ -1,0 +1,133 @@
+"""One rank of bench.py's C4 job on the GPU (TEST INFRASTRUCTURE): its LPT
+shard of a fixed multi-seed job over a small genome, the chains through the HIP
+path (DeviceChains), per-site posterior counts on the device, summed over the
+ranks by torch.distributed ("gloo": several ranks may share one GPU).
+
+    python tests/c4_rank.py --rank R --world W --port P --out counts.npz
+
+Used by tests/test_gpu_c4_sharded.py, which starts the ranks as fresh
+processes before they touch the GPU."""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+N_SITES, K, M, B, S, SEEDS = 30_000, 6, 50, 25, 4, 3
+SEG, BUF = 4_000, 200
+
+
+def problem():
+    from hygeia_amd import synthetic
+
+    segs = synthetic.segment_chains(synthetic.chromosome_sizes(N_SITES, n_chrom=3), SEG, BUF)
+    d = synthetic.simulate(N_SITES, S, S, K=K, seed=44, coverage=100.0)
+    return segs, d
+
+
+def job_args():
+    return argparse.Namespace(job="c4", seeds=2, total_seeds=SEEDS)
+
+
+def rank_counts(rank: int, world: int):
+    """This rank's chains on the GPU -> (counts [N_SITES][1+2K] int32 on the CPU, units)."""
+    import torch
+
+    import bench
+    from hygeia_amd import parallel, synthetic, two_group
+
+    segs, d = problem()
+    chains, n_out, units, _ = bench.build_chains(job_args(), segs, rank, world)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(d[k]).view(np.int16)).to(dev) for k in
+         ("meth_control", "tot_control", "meth_case", "tot_case")}
+    mu, sg = synthetic.regime_params(K)
+    model = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(K, 0.8), num_resampled_ancestors=M,
+                                       num_samples_backward=B,
+                                       max_total_reads=int(max(d["tot_control"].max(), d["tot_case"].max())),
+                                       max_duration=SEG + 2 * BUF)
+    dc = two_group.DeviceChains(model, chains, n_out, device=dev)
+    E = dc.emission(t["meth_control"], t["tot_control"], t["meth_case"], t["tot_case"])
+    dc.run(E)
+    torch.cuda.synchronize()
+    if not bool((dc.status == 0).all().item()):
+        raise RuntimeError(f"chains failed: {dc.status.cpu().numpy()}")
+    seg_of = {(ci << 32) | b: (s0, r0, rl) for (ci, b, s0, n, r0, rl) in segs}
+    src = np.concatenate([np.arange(c[4] + seg_of[c[3]][1], c[4] + seg_of[c[3]][1] + seg_of[c[3]][2]) for c in chains])
+    dst = np.concatenate([np.arange(seg_of[c[3]][0] + seg_of[c[3]][1], seg_of[c[3]][0] + seg_of[c[3]][1]
+                                    + seg_of[c[3]][2]) for c in chains])
+    counts = parallel.posterior_counts(dc.split_probs, dc.regime_probs, B, torch.from_numpy(src).to(dev),
+                                       torch.from_numpy(dst).to(dev), N_SITES)
+    threads = int(__import__("hygeia_amd._lib", fromlist=["load"]).load().hyg_tg_threads_per_chain(
+        model.handle, len(chains)))
+    return counts.cpu(), units, len(chains), threads
+
+
+def oracle_counts():
+    """The same job's counts from the CPU oracle's chains (test infrastructure)."""
+    import concurrent.futures as cf
+
+    import torch
+
+    import bench
+    from hygeia_amd import parallel, synthetic
+    from oracle import binding as ob
+
+    segs, d = problem()
+    chains, n_out, units, _ = bench.build_chains(job_args(), segs, 0, 1)
+    mu, sg = synthetic.regime_params(K)
+    p = ob.make_params(K=K, M=M, B=B, mu=mu, sigma=sg)
+    E = ob.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    split = torch.zeros(n_out, dtype=torch.float32)
+    regime = torch.zeros((n_out, 2 * K), dtype=torch.float32)
+
+    def one(c):
+        s0, n, sd, cid, o = c
+        return c, ob.chain(p, E[s0:s0 + n], sd, cid)
+
+    with cf.ThreadPoolExecutor(max_workers=8) as ex:
+        for (s0, n, sd, cid, o), out in ex.map(one, chains):
+            assert out["status"] == 0
+            split[o:o + n] = torch.from_numpy(out["split_probs"])
+            regime[o:o + n] = torch.from_numpy(out["regime_probs"])
+    seg_of = {(ci << 32) | b: (s0, r0, rl) for (ci, b, s0, n, r0, rl) in segs}
+    src = np.concatenate([np.arange(c[4] + seg_of[c[3]][1], c[4] + seg_of[c[3]][1] + seg_of[c[3]][2]) for c in chains])
+    dst = np.concatenate([np.arange(seg_of[c[3]][0] + seg_of[c[3]][1], seg_of[c[3]][0] + seg_of[c[3]][1]
+                                    + seg_of[c[3]][2]) for c in chains])
+    return parallel.posterior_counts(split, regime, B, torch.from_numpy(src), torch.from_numpy(dst), N_SITES), units
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--port", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+
+    from hygeia_amd import parallel
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(a.port)
+    dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
+    try:
+        counts, units, n_chains, threads = rank_counts(a.rank, a.world)
+        parallel.allreduce_counts(counts)
+        uu = torch.tensor([units, n_chains], dtype=torch.int64)
+        dist.all_reduce(uu)
+        if a.rank == 0:
+            np.savez(a.out, counts=counts.numpy(), units=int(uu[0].item()), chains=int(uu[1].item()),
+                     threads=threads)
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

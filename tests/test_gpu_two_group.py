@@ -83,6 +83,70 @@ def test_chain_bit_exact(oracle, K, M, B, T, S, cov, dseed, seed):
     np.testing.assert_array_equal(fw, ref["final_log_weights"])
 
 
+WIDTHS = [256, 384, 512, 768]
+
+
+@pytest.fixture
+def force_width():
+    """Pins the chain workgroup size (hyg_tg_force_threads) for one test and
+    restores the automatic choice afterwards."""
+    from hygeia_amd import _lib
+
+    L = _lib.load()
+
+    def set_width(fwd, bwd=None):
+        _lib.check(L.hyg_tg_force_threads(fwd, fwd if bwd is None else bwd))
+
+    yield set_width
+    L.hyg_tg_force_threads(0, 0)
+
+
+@pytest.mark.parametrize("width", WIDTHS)
+@pytest.mark.parametrize("case", [0, 1, 2, 4, 9, 10])
+def test_chain_bit_exact_every_width(oracle, force_width, width, case):
+    """Every chain-kernel width computes the same bits: 256 threads (three
+    chains per CU, C3 on one GPU), 384 (two per CU), 768 (one per CU: an 8-GPU
+    rank) and 512 (the C5 width), forward and backward (bwd at the same
+    width, and the 256-thread backward behind a wide forward)."""
+    from hygeia_amd import two_group
+
+    K, M, B, T, S, cov, dseed, seed = CASES[case]
+    mu, sg, theta, d, p = _setup(oracle, K, M, B, T, S, cov, dseed)
+    E = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    ref = oracle.chain(p, E, seed, 1000 + seed)
+    maxr = int(max(d["tot_control"].max(), d["tot_case"].max()))
+    model = _model(mu, sg, theta, M, B, maxr, T + 5)
+    for bwd in (width, 256):
+        force_width(width, bwd)
+        res, fw, ex = two_group.run({"control": d["meth_control"], "case": d["meth_case"]},
+                                    {"control": d["tot_control"], "case": d["tot_case"]}, model, seed, 1000 + seed)
+        pr = res.particle
+        np.testing.assert_array_equal(pr["merged_state"], ref["merged"])
+        np.testing.assert_array_equal(pr["control_state"], ref["control"])
+        np.testing.assert_array_equal(pr["case_state"], ref["case"])
+        np.testing.assert_array_equal(ex["split_probs"], ref["split_probs"])
+        np.testing.assert_array_equal(ex["regime_probs"], ref["regime_probs"])
+        assert ex["log_z"] == ref["log_z"]
+        np.testing.assert_array_equal(fw, ref["final_log_weights"])
+
+
+def test_width_selection_by_chains_per_cu():
+    """The automatic width: 768 threads up to one chain per CU, 384 up to two,
+    256 beyond (C3 on one GPU), 512 for the C5 shape whose LDS allows one."""
+    from hygeia_amd import _lib, synthetic as syn, two_group
+
+    L = _lib.load()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    mu, sg = syn.regime_params(6)
+    m6 = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(6), max_total_reads=200, max_duration=100)
+    assert [L.hyg_tg_threads_per_chain(m6.handle, n) for n in (1, cus, cus + 1, 2 * cus, 2 * cus + 1, 582)] == \
+        [768, 768, 384, 384, 256, 256 if 582 > 2 * cus else 384]
+    mu, sg = syn.regime_params(12)
+    m12 = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(12), max_total_reads=200, max_duration=100)
+    assert L.hyg_tg_threads_per_chain(m12.handle, 10) == 512
+    assert L.hyg_tg_threads_per_chain(m12.handle, 1164) == 512
+
+
 def test_zero_coverage_stretch(oracle):
     """Missing data (n = 0 for every sample) contributes exactly 0 (TFP BB at n=0)."""
     from hygeia_amd import two_group
