@@ -234,10 +234,13 @@ __device__ __forceinline__ int wave_incl_int(int v) {
 }
 
 // ---- combining the per-wave partials of a block reduction
-// Up to 4 waves: every lane reads all of them from LDS (broadcast reads) and
-// adds them in wave order. More waves (384 / 768-thread chains): lane l < NW
-// reads wave l's partial and a DPP row reduction / scan combines them, so the
-// registers and instructions do not grow with the workgroup (NW <= 16).
+// Up to HYG_SEQ_WAVES waves: every lane reads all of them from LDS (broadcast
+// reads) and adds them in wave order. More waves (768-thread chains): lane
+// l < NW reads wave l's partial and a DPP row reduction / scan combines them,
+// so the registers and instructions do not grow with the workgroup (NW <= 16).
+#ifndef HYG_SEQ_WAVES
+#define HYG_SEQ_WAVES 4
+#endif
 template <int CTRL>
 __device__ __forceinline__ hyg_u192 dpp192f(hyg_u192 v) {
   hyg_u192 r;
@@ -262,7 +265,7 @@ __device__ __forceinline__ hyg_u128 row_sum128(hyg_u128 v) {
 template <int NW>
 __device__ __forceinline__ hyg_u192 sum_waves192(const hyg_u192* r) {
   static_assert(NW >= 1 && NW <= 16, "waves per workgroup");
-  if constexpr (NW <= 4) {
+  if constexpr (NW <= HYG_SEQ_WAVES) {
     hyg_u192 s = r[0];
     for (int w = 1; w < NW; ++w) s = hyg_u192_add(s, r[w]);
     return s;
@@ -276,7 +279,7 @@ __device__ __forceinline__ hyg_u192 sum_waves192(const hyg_u192* r) {
 template <int NW>
 __device__ __forceinline__ hyg_u128 sum_waves128(const hyg_u128* r) {
   static_assert(NW >= 1 && NW <= 16, "waves per workgroup");
-  if constexpr (NW <= 4) {
+  if constexpr (NW <= HYG_SEQ_WAVES) {
     hyg_u128 s = r[0];
     for (int w = 1; w < NW; ++w) s = hyg_u128_add(s, r[w]);
     return s;
@@ -307,7 +310,7 @@ __device__ __forceinline__ void block_max_cnt(double m, int c, unsigned char* re
     ((int*)red)[4 * wave_id() + 2] = c;
   }
   lds_barrier();
-  if constexpr (NT / 64 <= 4) {
+  if constexpr (NT / 64 <= HYG_SEQ_WAVES) {
     double mm = ((double*)red)[0];
     int cc = ((int*)red)[2];
     for (int w = 1; w < NT / 64; ++w) {
@@ -341,7 +344,7 @@ __device__ __forceinline__ double block_max(double v, unsigned char* red) {
   lds_barrier();
   if (lane_id() == 0) ((double*)red)[wave_id()] = v;
   lds_barrier();
-  if constexpr (NT / 64 <= 4) {
+  if constexpr (NT / 64 <= HYG_SEQ_WAVES) {
     double m = ((double*)red)[0];
     for (int w = 1; w < NT / 64; ++w) m = dmax(m, ((double*)red)[w]);
     return m;
@@ -389,7 +392,7 @@ __device__ __forceinline__ hyg_u192 block_excl192(hyg_u192 v, unsigned char* red
   if (lane_id() == 0) r[wave_id()] = wt;
   lds_barrier();
   hyg_u192 pre = hyg_u192_zero(), tot = hyg_u192_zero();
-  if constexpr (NT / 64 <= 4) {
+  if constexpr (NT / 64 <= HYG_SEQ_WAVES) {
     for (int w = 0; w < NT / 64; ++w) {
       if (w < wave_id()) pre = hyg_u192_add(pre, r[w]);
       tot = hyg_u192_add(tot, r[w]);
@@ -431,7 +434,7 @@ __device__ __forceinline__ void block_scan128(hyg_u128 v, hyg_u128* out, unsigne
   if (lane_id() == 0) r[wave_id()] = wt;
   lds_barrier();
   hyg_u128 pre = hyg_u128_zero(), tot = hyg_u128_zero();
-  if constexpr (NT / 64 <= 4) {
+  if constexpr (NT / 64 <= HYG_SEQ_WAVES) {
     for (int w = 0; w < NT / 64; ++w) {
       if (w < wave_id()) pre = hyg_u128_add(pre, r[w]);
       tot = hyg_u128_add(tot, r[w]);

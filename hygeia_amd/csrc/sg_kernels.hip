@@ -553,7 +553,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
     return;
   }
   double logZ =
-      mx0 + hyg_log(hyg_u128_to_f64(block_sum128<NB>(hyg_fix100(hyg_exp(my_lw - mx0)), red), 100));
+      mx0 + hyg_log(hyg_u128_to_f64(block_sum128<NB>(hyg_exp_fix100(my_lw - mx0), red), 100));
   double my_w = (tid < K) ? hyg_exp(my_lw - logZ) : 0.0;
   if (tid < K) {
     st_[tid] = my_st;
@@ -725,7 +725,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
               // T_j = (j + u) / L <= Q_i as exact C_i >= ceil(T_j R)
               const bool inres = tid >= Kk && tid < Np;
               const double rmax = block_max<NB>(inres ? lq : HYG_NINF, red);
-              const hyg_u128 m2 = inres ? hyg_fix100(hyg_exp(lq - rmax)) : hyg_u128_zero();
+              const hyg_u128 m2 = inres ? hyg_exp_fix100(lq - rmax) : hyg_u128_zero();
               block_scan128<NB>(m2, cum, red);
               const hyg_u128 incl = hyg_u128_add(cum[tid], m2);
               lds_barrier();
@@ -888,7 +888,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       }
       {
         hyg_u128 fx = hyg_u128_zero();
-        if ((NB == NT) || wv < NT / 64) fx = hyg_fix100(hyg_exp(nlw - mx));  // waves >= 4 hold no particle
+        if ((NB == NT) || wv < NT / 64) fx = hyg_exp_fix100(nlw - mx);  // waves >= 4 hold no particle
         logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NB>(fx, red), 100));
       }
       if (tid == 0) sg_st4(ctl, (unsigned)t);  // records 0 .. t-1 are published

@@ -13,7 +13,7 @@ constexpr int kDefaultThreads = 256;     // forward workgroup size
 constexpr int kDefaultThreadsBwd = 256;  // backward workgroup size (HYG_THREADS[_FWD/_BWD] override)
 // forward / backward workgroup size when a launch has at most one chain per CU
 // (tg_kernels.hip threads_per_chain; HYG_LOWOCC_THREADS overrides the forward's)
-constexpr int kLowOccThreads = 768;
+constexpr int kLowOccThreads = 512;
 constexpr int kEBlock = 8;     // emission rows staged in LDS per block of steps
 
 // Device-side chain descriptor (lives in the workspace header).

@@ -69,15 +69,17 @@ __device__ __forceinline__ int fdiv(int n, int d, float rd) {
   return q;
 }
 
-// hyg_fix100(hyg_exp(x[i])) for R values at once, written statement by
-// statement across the values: the same operations in the same order per
-// value as include/hyg_arith.h (so the same bits), but the R dependent f64
-// chains sit side by side in the instruction stream. Written as one function
-// per value, the compiler schedules the chains one after another and every
-// f64 operation waits for its predecessor's result.
+// hyg_exp_fix100(x[i]) (= hyg_fix100(hyg_exp(x[i])), include/hyg_arith.h) for R
+// values at once, written statement by statement across the values: the same
+// operations in the same order per value (so the same bits), but the R
+// dependent f64 chains sit side by side in the instruction stream. Written as
+// one function per value, the compiler schedules the chains one after another
+// and every f64 operation waits for its predecessor's result. The image is
+// formed from the polynomial value and the exponent by shifts (no scaling by
+// 2^k, no float floors).
 template <int R>
 __device__ __forceinline__ void exp_fix100_lockstep(const double (&x)[R], hyg_u128 (&out)[R]) {
-  double xc[R], kd[R], r[R], r2[R], r4[R], r8[R], p[R], v[R];
+  double xc[R], kd[R], r[R], r2[R], r4[R], r8[R], p[R];
   int k[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) xc[i] = __builtin_fmin(__builtin_fmax(x[i], -746.0), 710.0);
@@ -113,37 +115,7 @@ __device__ __forceinline__ void exp_fix100_lockstep(const double (&x)[R], hyg_u1
     p[i] = u0 + u1 * r8[i];
   }
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int big = k[i] > 1023, sub = k[i] < -1021;
-    const int k1 = big ? k[i] - 1 : (sub ? k[i] + 54 : k[i]);
-    const double p1 = big ? p[i] * 2.0 : p[i];
-    double w = p1 * hyg_pow2(k1);
-    w = sub ? w * 5.5511151231257827021e-17 : w;
-    w = (x[i] < -745.13321910194110842) ? 0.0 : w;
-    w = (x[i] > 709.782712893383973096) ? HYG_INF : w;
-    v[i] = (x[i] != x[i]) ? x[i] : w;
-  }
-  // hyg_fix100, statement by statement
-  double hf[R], lf[R], lhf[R], llf[R], hhf[R], hlf[R];
-#pragma unroll
-  for (int i = 0; i < R; ++i) v[i] = (v[i] > 0.0 && v[i] < 65536.0) ? v[i] * 0x1p100 : 0.0;
-#pragma unroll
-  for (int i = 0; i < R; ++i) hf[i] = __builtin_floor(v[i] * 0x1p-64);
-#pragma unroll
-  for (int i = 0; i < R; ++i) lf[i] = v[i] - hf[i] * 0x1p64;
-#pragma unroll
-  for (int i = 0; i < R; ++i) lhf[i] = __builtin_floor(lf[i] * 0x1p-32);
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    llf[i] = lf[i] - lhf[i] * 0x1p32;
-    hhf[i] = __builtin_floor(hf[i] * 0x1p-32);
-  }
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    hlf[i] = hf[i] - hhf[i] * 0x1p32;
-    out[i].lo = ((uint64_t)(uint32_t)lhf[i] << 32) | (uint64_t)(uint32_t)llf[i];
-    out[i].hi = ((uint64_t)(uint32_t)hhf[i] << 32) | (uint64_t)(uint32_t)hlf[i];
-  }
+  for (int i = 0; i < R; ++i) out[i] = hyg_exp_fix100_pk(p[i], k[i], x[i]);
 }
 
 // --------------------------------------------------------------- model
@@ -596,7 +568,7 @@ __device__ __forceinline__ double log_mass_sum(const double* W, int N, double mx
 #pragma unroll 4
   for (int n = threadIdx.x; n < N; n += NT) {
     const double x = W[n] - mx;
-    if (x >= -70.0) s = hyg_u128_add(s, hyg_fix100(hyg_exp(x)));  // exp(x < -70) < 2^-100 -> 0
+    s = hyg_u128_add(s, hyg_exp_fix100(x));  // exp(x < -70) < 2^-100 -> 0
   }
   const hyg_u128 S = block_sum128<NT>(s, red);
   return hyg_log(hyg_u128_to_f64(S, 100));
@@ -613,7 +585,7 @@ __device__ __forceinline__ void categorical_block(int N, double lmax, LogitFn lo
   hyg_u128 loc = hyg_u128_zero();
   for (int n = p0; n < p1; ++n) {
     const double x = logit(n) - lmax;
-    if (x >= -70.0) loc = hyg_u128_add(loc, hyg_fix100(hyg_exp(x)));
+    loc = hyg_u128_add(loc, hyg_exp_fix100(x));
   }
   block_scan128<NT>(loc, cp, red);
   lds_barrier();
@@ -632,7 +604,7 @@ __device__ __forceinline__ void categorical_block(int N, double lmax, LogitFn lo
       const int a0 = ch * cs, a1 = (a0 + cs < N) ? a0 + cs : N;
       for (int n = a0; n < a1; ++n) {
         const double x = logit(n) - lmax;
-        if (x >= -70.0) cdf = hyg_u128_add(cdf, hyg_fix100(hyg_exp(x)));
+        cdf = hyg_u128_add(cdf, hyg_exp_fix100(x));
         if (hyg_u128_lt(target, cdf)) { sel = n; break; }
       }
     }
@@ -1323,9 +1295,10 @@ tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
   }
 }
 
-// Three waves per SIMD (<= 168 VGPRs) at 256, 384 and 768 threads: a CU holds
-// three, two or one chain(s) (the second argument is the minimum waves per
-// SIMD); 512 threads (the C5 kernel, one chain per CU by its LDS) may use 256.
+// Three waves per SIMD (<= 168 VGPRs) at 256 and 768 threads: a CU holds three
+// chains or one (the second argument is the minimum waves per SIMD); 512
+// threads (one chain per CU: C5 by its LDS, or a low-occupancy launch) may use
+// up to 256 VGPRs.
 template <int NT, int KC = 0, int MC = 0, int BC = 0, bool PHS = false>  // PHS: phase-timer build
 __global__ void __launch_bounds__(NT, (NT == 512 ? 1 : 3))
 tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
@@ -2129,7 +2102,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             }
             const double lmax = wave_max(sv);
             hyg_u128 ms = hyg_u128_zero();
-            if (v) ms = hyg_fix100(hyg_exp(sv - lmax));
+            if (v) ms = hyg_exp_fix100(sv - lmax);
             const hyg_u128 cdf = wave_incl128(ms);
             hyg_u128 total;
             total.lo = rdlane64(cdf.lo, L - 1);
@@ -2282,18 +2255,18 @@ int device_cus() {
   return cus;
 }
 // Threads per chain workgroup. HYG_THREADS (or HYG_THREADS_FWD / _BWD) if set.
-// Otherwise by what the launch's chains leave of the GPU. The pipeline-shape
-// kernels keep three waves per SIMD (<= 168 VGPRs, no spills) at every width,
-// so a CU holds k chains of 768 / k threads:
+// Otherwise by what the launch's chains leave of the GPU:
 //  - the forward's LDS at 256 threads already forces one workgroup per CU
 //    (K = 12, C5: 145 KB): 512, twice the waves on the CU's one chain;
 //  - at most one chain per CU (e.g. an 8-GPU rank of the C3 job, 73 chains):
-//    768 threads (kLowOccThreads), whose extra waves shorten each step of the
-//    sequential chain;
-//  - at most two per CU (an 8-GPU rank of C4, 291 chains): 384;
-//  - else 256, three chains per CU (C3 on one GPU: 582 chains).
+//    kLowOccThreads, whose extra waves shorten the parallel phases of each
+//    step of the sequential chain (HYG_LOWOCC_THREADS: 256, 512 or 768);
+//  - else 256, up to three chains per CU (<= 168 VGPRs: C3 on one GPU, 582
+//    chains; an 8-GPU rank of C4, 291). A 384-thread workgroup does not buy
+//    two chains per CU: its six waves land 2-2-1-1 on the SIMDs, so a second
+//    one would need four waves on a SIMD that holds three.
 int g_force_threads[2] = {0, 0};  // hyg_tg_force_threads (tests): forward, backward; 0 = automatic
-bool valid_width(int x) { return x == 64 || x == 128 || x == 256 || x == 384 || x == 512 || x == 768; }
+bool valid_width(int x) { return x == 64 || x == 128 || x == 256 || x == 512 || x == 768; }
 int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
   if (g_force_threads[backward ? 1 : 0]) return g_force_threads[backward ? 1 : 0];
   static int env[2] = {-1, -1};
@@ -2308,16 +2281,14 @@ int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
   if (lowocc < 0) {
     const char* v = getenv("HYG_LOWOCC_THREADS");
     const int x = v ? atoi(v) : 0;
-    lowocc = (x == 256 || x == 384 || x == 512 || x == 768) ? x : kLowOccThreads;
+    lowocc = (x == 256 || x == 512 || x == 768) ? x : kLowOccThreads;
   }
   if (env[k]) return env[k];
   const int def = backward ? kDefaultThreadsBwd : kDefaultThreads;
   const size_t lds = make_layout(c.K, c.M, c.B, c.Nmax, def, false).total;
   if (2 * lds > 160 * 1024) return 512;
   if (c.M > 64) return def;  // the wider kernels assume the pipeline's M <= 64 (one ancestor per lane)
-  const int cus = device_cus();
-  if (n_chains <= cus) return lowocc;
-  if (n_chains <= 2 * cus) return 384;
+  if (n_chains <= device_cus()) return lowocc;
   return def;
 }
 }  // namespace
@@ -2394,7 +2365,7 @@ FwdFn fwd_kernel(const hyg_tg_consts& c) {
       return &tg_forward_kernel<NT, 0, 0, 0, true>;
     }
   }
-  if constexpr (NT == 256 || NT == 384 || NT == 512 || NT == 768)
+  if constexpr (NT == 256 || NT == 512 || NT == 768)
     if (shape_specialised(c)) return &tg_forward_kernel<NT, 6, 50, 25>;
   if constexpr (NT == 512)
     if (shape_c5(c)) return &tg_forward_kernel<512, 12, 50, 25>;
@@ -2408,7 +2379,7 @@ BwdFn bwd_kernel(const hyg_tg_consts& c) {
       return &tg_backward_kernel<NT, 0, 0, 0, true>;
     }
   }
-  if constexpr (NT == 256 || NT == 384 || NT == 512 || NT == 768)
+  if constexpr (NT == 256 || NT == 512 || NT == 768)
     if (shape_specialised(c)) return &tg_backward_kernel<NT, 6, 50, 25>;
   if constexpr (NT == 512)
     if (shape_c5(c)) return &tg_backward_kernel<512, 12, 50, 25>;
@@ -2518,7 +2489,6 @@ int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* ch
     case 64: rc = launch_forward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     case 128: rc = launch_forward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     case 256: rc = launch_forward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s); break;
-    case 384: rc = launch_forward_nt<384>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     case 768: rc = launch_forward_nt<768>(md, c, chains_dev, n_chains, E, ws, out, s); break;
     default: rc = launch_forward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s); break;
   }
@@ -2527,7 +2497,6 @@ int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* ch
     case 64: return launch_backward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s);
     case 128: return launch_backward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s);
     case 256: return launch_backward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s);
-    case 384: return launch_backward_nt<384>(md, c, chains_dev, n_chains, E, ws, out, s);
     case 768: return launch_backward_nt<768>(md, c, chains_dev, n_chains, E, ws, out, s);
     default: return launch_backward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s);
   }

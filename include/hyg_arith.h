@@ -262,6 +262,53 @@ HYG_HD hyg_u128 hyg_fix100(double e) {
   return r;
 }
 
+/* hyg_fix100(hyg_exp(x)), the same integer computed from the pieces of the
+ * exponential instead of through its double value: for -70 <= x < 11,
+ * hyg_exp(x) = p 2^k exactly (the polynomial value p, a normal double in
+ * (0.7, 1.42), scaled by a power of two without rounding), so
+ * floor(e 2^100) = m 2^(E_p + k + 48) for p's 53-bit significand m and exponent
+ * E_p -- a shift, no float floors. Below -70 the exact image is 0
+ * (e^x 2^100 < 1 for x < -69.32); x >= 11 (e >= 65536 is 0 in hyg_fix100) does
+ * not occur on the paths that use it (x <= 0) and is also mapped to 0.
+ * tests/test_arith.py checks the two forms integer for integer. */
+HYG_HD hyg_u128 hyg_exp_fix100_pk(double p, int k, double x) {
+  const uint64_t pb = hyg_f64_bits(p);
+  const int sh = (int)((pb >> 52) & 0x7ff) - 1023 + k + 48; /* in [-54, 64] on the range */
+  const uint64_t m = (pb & 0x000fffffffffffffull) | 0x0010000000000000ull;
+  const int shp = sh > 0 ? sh : 0, shn = sh < 0 ? -sh : 0;
+  const uint64_t mr = m >> (shn & 63);
+  const int in = (x >= -70.0) && (x < 11.0);
+  hyg_u128 r;
+  r.lo = (!in || shp >= 64) ? 0 : (mr << (shp & 63));
+  r.hi = (!in || shp == 0) ? 0 : ((shp >= 64) ? mr : (mr >> ((64 - shp) & 63)));
+  return r;
+}
+HYG_HD hyg_u128 hyg_exp_fix100(double x) {
+  const double xc = HYG_FMIN(HYG_FMAX(x, -746.0), 710.0);
+  const double kd = HYG_FLOOR(xc * HYG_INV_LN2 + 0.5);
+  const int k = (int)kd;
+  const double hi = xc - kd * HYG_LN2_HI;
+  const double lo = kd * HYG_LN2_LO;
+  const double r = hi - lo;
+  const double r2 = r * r;
+  const double r4 = r2 * r2;
+  const double r8 = r4 * r4;
+  const double q0 = 1.0 + 1.0 * r;
+  const double q1 = 0.5 + 1.6666666666666665741e-01 * r;
+  const double q2 = 4.1666666666666664354e-02 + 8.3333333333333332177e-03 * r;
+  const double q3 = 1.3888888888888888889e-03 + 1.9841269841269841253e-04 * r;
+  const double q4 = 2.4801587301587301566e-05 + 2.7557319223985890653e-06 * r;
+  const double q5 = 2.7557319223985890653e-07 + 2.5052108385441718775e-08 * r;
+  const double q6 = 2.0876756987868098979e-09 + 1.6059043836821614599e-10 * r;
+  const double s0 = q0 + q1 * r2;
+  const double s1 = q2 + q3 * r2;
+  const double s2 = q4 + q5 * r2;
+  const double u0 = s0 + s1 * r4;
+  const double u1 = s2 + q6 * r4;
+  const double p = u0 + u1 * r8;
+  return hyg_exp_fix100_pk(p, k, x);
+}
+
 /* value * 2^-scale as a double: the top 53 bits (truncated), exact scaling. */
 HYG_HD double hyg_u128_to_f64(hyg_u128 a, int scale) {
   int p; uint64_t top;

@@ -107,15 +107,16 @@ void hyg_tg_model_destroy(hyg_tg_model* model);
 int32_t hyg_tg_num_particles(const hyg_tg_model* model);
 
 /* Threads per chain workgroup of the forward kernel for a launch of n_chains
- * chains on the current device: 256 (three chains per CU), 512 (up to 1.25
- * chains per CU) or the low-occupancy width (at most one chain per CU), whose
- * extra waves shorten each step of the sequential chain. Diagnostic: the
- * launch functions choose it themselves. No reference counterpart (the
- * reference runs one chain per CPU process, modules/two_group/4_infer.nf:28). */
+ * chains on the current device: 256 (up to three chains per CU) or, at most
+ * one chain per CU, the low-occupancy width 512, whose extra waves shorten the
+ * parallel phases of each step of the sequential chain (512 also for the
+ * K = 12 stress shape, one chain per CU by its LDS). Diagnostic: the launch
+ * functions choose it themselves. No reference counterpart (the reference
+ * runs one chain per CPU process, modules/two_group/4_infer.nf:28). */
 int32_t hyg_tg_threads_per_chain(const hyg_tg_model* model, int32_t n_chains);
 
 /* Test / tuning override of the chain workgroup sizes for every later launch
- * in the process: forward and backward threads (64, 128, 256, 384, 512 or 768;
+ * in the process: forward and backward threads (64, 128, 256, 512 or 768;
  * 0 = the automatic choice above). Not thread-safe. The results do not depend
  * on it: every width computes the same bits. */
 int hyg_tg_force_threads(int32_t forward, int32_t backward);

@@ -135,8 +135,11 @@ static double xsum(const double* v, int n) {
   return hyg_u128_to_f64(s, 100);
 }
 
-/* descending by value, ties by ascending index (arma::sort_index "descend") */
-static const double* g_sort_v;
+/* descending by value, ties by ascending index (arma::sort_index "descend").
+ * The comparator's key array is thread-local: the tests and the CPU baselines
+ * run several chains at once in threads (a shared pointer let one thread's
+ * sort read another's weights). */
+static _Thread_local const double* g_sort_v;
 static int cmp_desc(const void* a, const void* b) {
   const int i = *(const int*)a, j = *(const int*)b;
   if (g_sort_v[i] > g_sort_v[j]) return -1;

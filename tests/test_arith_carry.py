@@ -139,3 +139,54 @@ def test_fix149f_low128_equals_fix149f_below_2_pow_minus_21(tmp_path):
         assert (lo, hi) == (w0, w1)
         n += 1
     assert n == 106 * 4 + 3000 + 2
+
+
+PROG_EXPFIX = r"""
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include "hyg_arith.h"
+static uint64_t st = 0x9E3779B97F4A7C15ull;
+static uint64_t nx() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; }
+static int check(double x) {
+  const hyg_u128 a = hyg_fix100(hyg_exp(x)), b = hyg_exp_fix100(x);
+  if (a.lo != b.lo || a.hi != b.hi) {
+    printf("MISMATCH %.17g %016llx %016llx %016llx %016llx\n", x, (unsigned long long)a.hi,
+           (unsigned long long)a.lo, (unsigned long long)b.hi, (unsigned long long)b.lo);
+    return 1;
+  }
+  return 0;
+}
+int main() {
+  int bad = 0, n = 0;
+  // uniform over the used range and beyond, dense near the cut points
+  for (int i = 0; i < 400000; ++i, ++n) bad += check(-80.0 + 80.0 * (double)(nx() >> 11) * 0x1p-53);
+  for (int i = 0; i < 100000; ++i, ++n) bad += check(-70.5 + 1.5 * (double)(nx() >> 11) * 0x1p-53);
+  for (int i = 0; i < 100000; ++i, ++n) bad += check(-1e-3 * (double)(nx() >> 11) * 0x1p-53);
+  // every reduction boundary k ln2 +- a few ulps
+  for (int k = -102; k <= 1; ++k)
+    for (int d = -4; d <= 4; ++d, ++n) {
+      double x = (k + 0.5) * 0.69314718055994530942;
+      uint64_t b; std::memcpy(&b, &x, 8); b += d; std::memcpy(&x, &b, 8);
+      bad += check(x);
+    }
+  const double sp[] = {0.0, -0.0, -70.0, -69.3147, -1e-300, -HUGE_VAL, NAN, 5.0, 10.9};
+  for (double x : sp) { bad += check(x); ++n; }
+  printf("N %d BAD %d\n", n, bad);
+  return bad != 0;
+}
+"""
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_exp_fix100_shift_form_equals_float_form(tmp_path):
+    """hyg_exp_fix100 (the kernels' shift-based image) is hyg_fix100(hyg_exp(x))
+    (the oracle's form) integer for integer on and around [-70, 0]."""
+    src = tmp_path / "expfix.hip"
+    exe = tmp_path / "expfix"
+    src.write_text(PROG_EXPFIX)
+    subprocess.run([HIPCC, "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(REPO, "include"), "-o",
+                    str(exe), str(src)], check=True, capture_output=True, timeout=300)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout[-2000:]
+    assert "BAD 0" in out.stdout

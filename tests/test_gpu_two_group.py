@@ -83,7 +83,7 @@ def test_chain_bit_exact(oracle, K, M, B, T, S, cov, dseed, seed):
     np.testing.assert_array_equal(fw, ref["final_log_weights"])
 
 
-WIDTHS = [256, 384, 512, 768]
+WIDTHS = [256, 512, 768]
 
 
 @pytest.fixture
@@ -104,10 +104,10 @@ def force_width():
 @pytest.mark.parametrize("width", WIDTHS)
 @pytest.mark.parametrize("case", [0, 1, 2, 4, 9, 10])
 def test_chain_bit_exact_every_width(oracle, force_width, width, case):
-    """Every chain-kernel width computes the same bits: 256 threads (three
-    chains per CU, C3 on one GPU), 384 (two per CU), 768 (one per CU: an 8-GPU
-    rank) and 512 (the C5 width), forward and backward (bwd at the same
-    width, and the 256-thread backward behind a wide forward)."""
+    """Every chain-kernel width computes the same bits: 256 threads (up to three
+    chains per CU, C3 on one GPU), 512 (one per CU: an 8-GPU rank; the C5
+    width) and 768, forward and backward (the backward at the same width, and
+    the 256-thread backward behind a wide forward)."""
     from hygeia_amd import two_group
 
     K, M, B, T, S, cov, dseed, seed = CASES[case]
@@ -131,16 +131,16 @@ def test_chain_bit_exact_every_width(oracle, force_width, width, case):
 
 
 def test_width_selection_by_chains_per_cu():
-    """The automatic width: 768 threads up to one chain per CU, 384 up to two,
-    256 beyond (C3 on one GPU), 512 for the C5 shape whose LDS allows one."""
+    """The automatic width: 512 threads up to one chain per CU, 256 beyond (C3
+    on one GPU, an 8-GPU rank of C4), 512 for the C5 shape whose LDS allows
+    one chain per CU anyway."""
     from hygeia_amd import _lib, synthetic as syn, two_group
 
     L = _lib.load()
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     mu, sg = syn.regime_params(6)
     m6 = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(6), max_total_reads=200, max_duration=100)
-    assert [L.hyg_tg_threads_per_chain(m6.handle, n) for n in (1, cus, cus + 1, 2 * cus, 2 * cus + 1, 582)] == \
-        [768, 768, 384, 384, 256, 256 if 582 > 2 * cus else 384]
+    assert [L.hyg_tg_threads_per_chain(m6.handle, n) for n in (1, cus, cus + 1, 582)] == [512, 512, 256, 256]
     mu, sg = syn.regime_params(12)
     m12 = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(12), max_total_reads=200, max_duration=100)
     assert L.hyg_tg_threads_per_chain(m12.handle, 10) == 512

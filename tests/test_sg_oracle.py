@@ -271,3 +271,25 @@ def test_golden_chain(sg, name):
     out = sg.chain(p, E, int(g["seed"]), int(g["chain_id"]))
     assert out["status"] == 0
     assert np.array_equal(out["regime_probs"], g["regime_probs"])
+
+
+def test_concurrent_chains_equal_sequential_runs():
+    """The oracle runs chains in threads (the GPU config tests, the CPU
+    baselines): concurrent chains must not share sort state. A shared qsort key
+    pointer made concurrently sorted chains read each other's weights."""
+    import concurrent.futures as cf
+
+    from hygeia_amd import synthetic as syn
+    from oracle import sg_binding as sgb
+
+    p = sgb.make_params(K=6)
+    runs = []
+    for i in range(4):
+        d = syn.simulate(6000, 2, 1, K=6, seed=300 + i, coverage=100.0, omega=syn.SG_OMEGA)
+        runs.append(sgb.emission(p, d["meth_control"], d["tot_control"]))
+    seq = [sgb.chain(p, E, seed=i, chain_id=9) for i, E in enumerate(runs)]
+    with cf.ThreadPoolExecutor(max_workers=4) as ex:
+        par = list(ex.map(lambda a: sgb.chain(p, a[1], seed=a[0], chain_id=9), enumerate(runs)))
+    for a, b in zip(seq, par):
+        assert a["status"] == b["status"] == 0
+        np.testing.assert_array_equal(a["regime_probs"], b["regime_probs"])

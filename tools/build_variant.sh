@@ -1,8 +1,12 @@
-# builds hygeia_amd/lib/libhygeia_amd_<name>.so: the library with extra compiler flags on tg_kernels.hip
-# usage: bash tools/build_variant.sh <name> <extra flags...>   (load it with HYG_LIB_PATH)
-name=$1; shift
-O=hygeia_amd/lib/obj
-F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt"
-/opt/rocm/bin/hipcc $F "$@" -c hygeia_amd/csrc/tg_kernels.hip -o /tmp/tg_$name.o &&
-objs=$(ls $O/*.o | grep -v tg_kernels) &&
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o hygeia_amd/lib/libhygeia_amd_$name.so /tmp/tg_$name.o $objs && echo built hygeia_amd/lib/libhygeia_amd_$name.so
+# An A/B build of the same sources with extra flags into hygeia_amd/lib/var_<tag>/
+# (select it with HYG_LIB_PATH=hygeia_amd/lib/var_<tag>/libhygeia_amd.so).
+# usage: bash tools/build_variant.sh <tag> -DNAME=VALUE ...
+tag=$1; shift
+D=hygeia_amd/lib/var_$tag
+mkdir -p $D
+F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt -w"
+for s in capi.cpp tg_kernels.hip sg_kernels.hip dmp_kernels.hip bed_kernels.hip pre_kernels.hip; do
+  /opt/rocm/bin/hipcc $F "$@" -c hygeia_amd/csrc/$s -o $D/$s.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libhygeia_amd.so $D/*.o && rm -f $D/*.o && echo $D/libhygeia_amd.so

@@ -7,7 +7,7 @@ O=gpurun_out/$tag
 mkdir -p $O
 ( nproc; python3 -c 'import os; print(len(os.sched_getaffinity(0)), os.environ.get("OMP_NUM_THREADS"))'; cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo ) > $O/host.txt 2>&1
 if [ "$2" != "skip-tests" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
   tail -2 $O/tests.log
 fi
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }

@@ -20,6 +20,7 @@ for cmd in "$@"; do
   timeout -k 10 600 bash -c "$cmd" > $O/b$i.json 2> $O/b$i.err
   rc=$?
   tail -c 600 $O/b$i.json
-  if [ $rc -ne 0 ]; then echo "bench $i rc=$rc: stop"; tail -5 $O/b$i.err; exit $rc; fi
+  if [ $rc -eq 1 ]; then echo "[$i] rc=1 (failure, not a crash)"; tail -5 $O/b$i.err; fi
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[$i] rc=$rc: stop"; tail -5 $O/b$i.err; exit $rc; fi
 done
 echo done
