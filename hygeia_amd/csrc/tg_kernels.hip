@@ -847,7 +847,7 @@ __device__ __forceinline__ void optimal_resample(const double* W, uint64_t* sort
   const float Lf = (float)L;
   const hyg_u192 R = sh.R, preK = sh.preK;
   for (int j = tid; j < L; j += NT) {
-    tau[j] = hyg_u192_add(preK, hyg_ceil_mul_f32(((float)j + U) / Lf, R));
+    tau[j] = hyg_u192_add(preK, hyg_ceil_mul_f32_bf(((float)j + U) / Lf, R));
     parents[Kk + j] = key_index(sorted[Kk]);  // unfilled -> residual index 0
   }
   for (int p = tid; p < Kk; p += NT) parents[p] = key_index(sorted[p]);
@@ -1105,7 +1105,7 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
       const int L = M - bb;
       const hyg_u192 preK = hyg_u192_sub(total, Rr);
       hyg_u192 tau = hyg_u192_zero();
-      if (lane < L) tau = hyg_u192_add(preK, hyg_ceil_mul_f32(((float)lane + Usys) / (float)L, Rr));
+      if (lane < L) tau = hyg_u192_add(preK, hyg_ceil_mul_f32_bf(((float)lane + Usys) / (float)L, Rr));
       const hyg_u192 tlast = rdlane192(tau, L > 0 ? L - 1 : 0);
       if (L > 0 && hasB && !hyg_u192_ge(massA, tlast)) {
         status = FAST_FALLBACK_REGEN;

@@ -509,6 +509,50 @@ HYG_HD hyg_u192 hyg_ceil_mul_f32(float T, hyg_u192 R) {
   return r;
 }
 
+/* hyg_ceil_mul_f32 without branches (the same integer: tests/test_arith_carry.py):
+ * the kernels evaluate it for a wave of systematic targets whose exponents
+ * differ lane to lane, so the branch form runs several of its shift paths
+ * one after another. m R from 24 x 32-bit partial products; the bias and the
+ * shift by s = 64 q + sb by word selects and one funnel shift. */
+HYG_HD hyg_u192 hyg_ceil_mul_f32_bf(float T, hyg_u192 R) {
+  const uint32_t b = hyg_f32_bits(T);
+  const int E = (int)((b >> 23) & 0xff);
+  const uint64_t m = (E == 0) ? (uint64_t)(b & 0x7fffffu) : (uint64_t)((b & 0x7fffffu) | 0x800000u);
+  const int s = (E == 0) ? 149 : 150 - E; /* in [23, 149] for 0 < T <= 1 */
+  /* m w = (m w_lo) + (m w_hi) 2^32 for each 64-bit word w of R (m < 2^24) */
+  const uint64_t a0 = m * (R.w0 & 0xffffffffu), b0 = m * (R.w0 >> 32);
+  const uint64_t a1 = m * (R.w1 & 0xffffffffu), b1 = m * (R.w1 >> 32);
+  const uint64_t a2 = m * (R.w2 & 0xffffffffu), b2 = m * (R.w2 >> 32);
+  const uint64_t l0 = a0 + (b0 << 32), h0 = (b0 >> 32) + (l0 < a0 ? 1u : 0u);
+  const uint64_t l1 = a1 + (b1 << 32), h1 = (b1 >> 32) + (l1 < a1 ? 1u : 0u);
+  const uint64_t l2 = a2 + (b2 << 32);
+  hyg_u192 P;
+  P.w0 = l0;
+  P.w1 = h0 + l1;
+  P.w2 = h1 + l2 + (P.w1 < h0 ? 1u : 0u);
+  /* ceil(P / 2^s) = (P + 2^s - 1) >> s */
+  const int q = s >> 6, sb = s & 63;
+  const uint64_t part = (sb == 0) ? 0 : ((1ull << (sb & 63)) - 1ull);
+  hyg_u192 bias;
+  bias.w0 = (q > 0) ? ~0ull : part;
+  bias.w1 = (q > 1) ? ~0ull : ((q == 1) ? part : 0);
+  bias.w2 = (q == 2) ? part : 0;
+  const hyg_u192 Q = hyg_u192_add(P, bias);
+  const uint64_t x0 = (q == 0) ? Q.w0 : ((q == 1) ? Q.w1 : Q.w2);
+  const uint64_t x1 = (q == 0) ? Q.w1 : ((q == 1) ? Q.w2 : 0);
+  const uint64_t x2 = (q == 0) ? Q.w2 : 0;
+  const int rs = (64 - sb) & 63;
+  hyg_u192 r;
+  r.w0 = (sb == 0) ? x0 : ((x0 >> sb) | (x1 << rs));
+  r.w1 = (sb == 0) ? x1 : ((x1 >> sb) | (x2 << rs));
+  r.w2 = (sb == 0) ? x2 : (x2 >> sb);
+  const int zero = (b == 0) || (b >> 31);
+  r.w0 = zero ? 0 : r.w0;
+  r.w1 = zero ? 0 : r.w1;
+  r.w2 = zero ? 0 : r.w2;
+  return r;
+}
+
 /* ------------------------------------------------------- Philox4x64-10 */
 typedef struct { uint64_t v[4]; } hyg_ph4;
 

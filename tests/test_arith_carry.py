@@ -190,3 +190,57 @@ def test_exp_fix100_shift_form_equals_float_form(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout[-2000:]
     assert "BAD 0" in out.stdout
+
+
+PROG_CEILMUL = r"""
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include "hyg_arith.h"
+static uint64_t st = 0x2545F4914F6CDD1Dull;
+static uint64_t nx() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; }
+int main() {
+  int bad = 0, n = 0;
+  for (int i = 0; i < 300000; ++i, ++n) {
+    float T;
+    const int kind = (int)(nx() & 3);
+    if (kind == 0) {  // the systematic targets ((j + U) / L in f32)
+      const int L = 1 + (int)(nx() % 64), j = (int)(nx() % (uint64_t)L);
+      const float U = (float)(nx() >> 40) * 0x1p-24f;
+      T = ((float)j + U) / (float)L;
+    } else if (kind == 1) {  // any float in [0, 1]
+      uint32_t b = (uint32_t)(nx() % 0x3f800001u);
+      std::memcpy(&T, &b, 4);
+    } else if (kind == 2) {  // subnormals and tiny values
+      uint32_t b = (uint32_t)(nx() % 0x01000000u);
+      std::memcpy(&T, &b, 4);
+    } else {
+      T = (nx() & 1) ? 1.0f : 0.0f;
+    }
+    hyg_u192 R{nx(), nx(), nx() & ((1ull << (nx() % 24)) - 1)};  // R < 2^151
+    if (nx() & 1) R.w2 = 0;
+    if ((nx() & 7) == 0) R.w1 = 0;
+    const hyg_u192 a = hyg_ceil_mul_f32(T, R), b = hyg_ceil_mul_f32_bf(T, R);
+    if (a.w0 != b.w0 || a.w1 != b.w1 || a.w2 != b.w2) {
+      if (bad < 5) printf("MISMATCH T=%a\\n", (double)T);
+      ++bad;
+    }
+  }
+  printf("N %d BAD %d\\n", n, bad);
+  return bad != 0;
+}
+"""
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_ceil_mul_branch_free_equals_branch_form(tmp_path):
+    """The kernels' branch-free exact systematic threshold (hyg_ceil_mul_f32_bf)
+    is the oracle's hyg_ceil_mul_f32, integer for integer."""
+    src = tmp_path / "ceilmul.hip"
+    exe = tmp_path / "ceilmul"
+    src.write_text(PROG_CEILMUL)
+    subprocess.run([HIPCC, "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(REPO, "include"), "-o",
+                    str(exe), str(src)], check=True, capture_output=True, timeout=300)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout[-2000:]
+    assert "BAD 0" in out.stdout
