@@ -41,6 +41,9 @@
 #define HYG_FLOOR(x) __builtin_floor(x)
 #define HYG_FMIN(a, b) __builtin_fmin(a, b)
 #define HYG_FMAX(a, b) __builtin_fmax(a, b)
+#define HYG_FLOORF(x) __builtin_floorf(x)
+#define HYG_FMINF(a, b) __builtin_fminf(a, b)
+#define HYG_FMAXF(a, b) __builtin_fmaxf(a, b)
 #else
 #include <math.h>
 #define HYG_HD static inline
@@ -53,9 +56,18 @@ static inline double hyg__floor(double v) {
 }
 static inline double hyg__fmin(double a, double b) { return (a < b) ? a : ((a != a) ? b : b); }
 static inline double hyg__fmax(double a, double b) { return (a > b) ? a : ((a != a) ? b : b); }
+static inline float hyg__floorf(float v) { /* |v| < 2^31 */
+  const float t = (float)(long long)v;
+  return (t > v) ? t - 1.0f : t;
+}
+static inline float hyg__fminf(float a, float b) { return (a < b) ? a : ((a != a) ? b : b); }
+static inline float hyg__fmaxf(float a, float b) { return (a > b) ? a : ((a != a) ? b : b); }
 #define HYG_FLOOR(x) hyg__floor(x)
 #define HYG_FMIN(a, b) hyg__fmin(a, b)
 #define HYG_FMAX(a, b) hyg__fmax(a, b)
+#define HYG_FLOORF(x) hyg__floorf(x)
+#define HYG_FMINF(a, b) hyg__fminf(a, b)
+#define HYG_FMAXF(a, b) hyg__fmaxf(a, b)
 #endif
 
 /* ------------------------------------------------------------------ bits */
@@ -171,8 +183,10 @@ HYG_HD double hyg_log(double x) {
  * subnormal ones; k > 127: (2p) 2^(k-1)), every step an IEEE f32 basic
  * operation, so host and device give the same bits. */
 HYG_HD float hyg_expf(float x) {
-  const float xc = (float)HYG_FMIN(HYG_FMAX((double)x, -104.0), 89.0); /* NaN -> -104 */
-  const float kf = (float)HYG_FLOOR((double)(xc * 0x1.715476p+0f + 0.5f));
+  /* (the clamp and the floor in f32: the same values as through double, since
+   * -104, 89 and the floor of an f32 value are f32 values) */
+  const float xc = HYG_FMINF(HYG_FMAXF(x, -104.0f), 89.0f); /* NaN -> -104 */
+  const float kf = HYG_FLOORF(xc * 0x1.715476p+0f + 0.5f);
   const float hi = xc - kf * 0x1.62e4p-1f;
   const float r = hi - kf * 0x1.7f7d1cp-20f;
   const float r2 = r * r;
