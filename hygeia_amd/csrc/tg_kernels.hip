@@ -338,7 +338,10 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
   size_t o = 0;
   l.W = o; o = align_up(o + sizeof(double) * l.npad, 16);
   if (backward) {
-    l.L = o; o = align_up(o + sizeof(double) * l.npad, 16);
+    // the backward's list / logit area is the weight area: the list path
+    // builds no weights and the general path turns the weights into logits
+    // in place
+    l.L = l.W;
     l.cp = o; o = align_up(o + sizeof(hyg_u128) * (NT + 1), 16);
   } else {
     // sort keys; the unbiased fallback reuses them as its (NT+1) x u128 prefix array
@@ -357,11 +360,14 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
     // per-wave partials of the top-set resampling path (counts per cutoff, mass)
     l.part = o; o = align_up(o + (sizeof(int) * kNCut + sizeof(hyg_u192)) * (NT / 64), 16);
   }
-  // the ancestors of the current step (single buffer: rewritten behind a barrier)
-  l.pst = o; o = align_up(o + sizeof(uint64_t) * M, 16);
-  l.pw = o; o = align_up(o + sizeof(double) * M, 16);
-  l.phz = o; o = align_up(o + sizeof(Hz4) * M, 16);
-  l.pf = o; o = align_up(o + sizeof(Pf3) * M, 16);
+  // the ancestors of the current step: one buffer in the forward (rewritten
+  // behind a barrier), two in the backward (record t in buffer t & 1 while
+  // record t-1 is stored into the other)
+  const size_t nb = backward ? 2 : 1;
+  l.pst = o; o = align_up(o + sizeof(uint64_t) * M * nb, 16);
+  l.pw = o; o = align_up(o + sizeof(double) * M * nb, 16);
+  l.phz = o; o = align_up(o + sizeof(Hz4) * M * nb, 16);
+  l.pf = o; o = align_up(o + sizeof(Pf3) * M * nb, 16);
   l.ering = o; o = align_up(o + sizeof(double) * 2 * kEBlock * 2 * K, 16);
   l.cl = o; o = align_up(o + const_lds_bytes(K), 16);
   l.parents = o; o = align_up(o + sizeof(int) * (M > B ? M : B), 16);
@@ -1804,16 +1810,17 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   auto rec_ptr = [&](int tt) { return rec0 + (size_t)tt * rstride; };
   StepScalars s = *(const StepScalars*)rec_ptr(T - 1);
   if (tid < s.n_par) {
+    const int o0 = ((T - 1) & 1) * M + tid;  // record t lives in LDS buffer t & 1
     const uint64_t* rst = (const uint64_t*)(rec_ptr(T - 1) + sizeof(StepScalars));
     const uint64_t st = rst[tid];
-    pst[tid] = st;
-    pw[tid] = ((const double*)(rst + M))[tid];
+    pst[o0] = st;
+    pw[o0] = ((const double*)(rst + M))[tid];
     const double2 hc = hz_at(md, K, 0, hyg_st_rc(st), hyg_st_dc(st));
     const double2 hk = hz_at(md, K, 1, hyg_st_rk(st), hyg_st_dk(st));
     Hz4 h;
     h.lrc = hc.x; h.l1c = hc.y; h.lrk = hk.x; h.l1k = hk.y;
-    phz[tid] = h;
-    pf[tid] = prefetch_rows(md, K, st);
+    phz[o0] = h;
+    pf[o0] = prefetch_rows(md, K, st);
   }
   // stage-1 registers: record t-1
   StepScalars s1{};
@@ -1836,24 +1843,27 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   if (dbg && tid == 0) ph_acc[kPh - 1] = __builtin_amdgcn_s_memtime();
 
   for (int t = T - 1; t >= 0; --t) {
-    // ---- regenerate the particles of step t from its record (in LDS)
+    // ---- regenerate the particles of step t from its record (LDS buffer t & 1;
+    //      record t-1 is stored into the other buffer during this step)
+    const int bt = t & 1;
     const double* Et = erow(ering, t, K2);
     const int np = s.n_par;
-    const uint64_t* P = pst;
-    const Hz4* PHZ = phz;
-    const Pf3* PF = pf;
+    const uint64_t* P = pst + bt * M;
+    const double* PW = pw + bt * M;
+    const Hz4* PHZ = phz + bt * M;
+    const Pf3* PF = pf + bt * M;
     const float rnp = (np > 0) ? 1.0f / (float)np : 0.0f;
     const int N = (s.mode == MODE_INIT) ? K * K : I * np;
     double mloc = HYG_NINF;
     int cloc = 0;
     // The rows of the backward kernel need the weights of the few candidates
-    // that can reach a trajectory's next state only; all N weights are built
-    // for the final step's draw and for the general paths.
+    // that can reach a trajectory's next state only (the list path); all N
+    // weights are built for the final step's draw and for the general path.
     const bool fast = (s.mode != MODE_INIT) && np <= 64 && B <= 64 && Nmax >= 192 && t != T - 1;
     bool w_ready = false;
     auto make_W = [&]() {
       if (s.mode == MODE_INIT) gen_weights_init<NT>(cl, K, s.r_ph, Et, W, &mloc, &cloc);
-      else gen_weights<NT>(cl, K, I, np, s.mode, s.log_c, s.lse, P, pw, PHZ, Et, W, &mloc, &cloc);
+      else gen_weights<NT>(cl, K, I, np, s.mode, s.log_c, s.lse, P, PW, PHZ, Et, W, &mloc, &cloc);
       w_ready = true;
     };
     if (!fast) make_W();
@@ -1880,7 +1890,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         w2 = ((const double*)(rst + M))[tid];
       }
     }
-    // ---- emission block t/EB - 2 into the half freed after this step
+    // ---- emission block t/EB - 2 into the half freed after this step's rows
     const bool eload = (t % kEBlock) == 0 && t >= 2 * kEBlock;
     constexpr int EQ = (kEBlock * 2 * HYG_KMAX + NT - 1) / NT;  // rows of one block per thread
     double ebuf[EQ];
@@ -1893,7 +1903,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         ebuf[q] = (i < e_tot) ? Ech[(size_t)t0 * K2 + i] : 0.0;
       }
     }
-    lds_barrier();
+    if (!fast) lds_barrier();  // W written by every thread (the list path reads only LDS written behind barriers)
     BPH(1);
     auto state_of = [&](int n) -> uint64_t {
       if (s.mode == MODE_INIT) return init_state(K, n);
@@ -1914,95 +1924,71 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     const bool pre_bits = B <= 64 && NT >= 128;
     if (pre_bits && t == T - 1 && t >= 1 && wave_id() == NT / 64 - 1)
       backward_bits(rb + ((t - 1) & 1) * rbs, B, t - 1, ch.seed, ch.chain_id);
+    auto rnd = [&](int b) -> uint64_t {
+      return hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
+    };
+    bool fail = false;
     if (t == T - 1) {
       // ---- B draws from the final weights (:383-385)
       const double lmax = block_max<NT>(mloc, red);
       if (!(lmax > HYG_NINF)) { if (tid == 0) sh.status = HYG_ENUMERIC; lds_barrier(); break; }
       auto logit = [&](int n) -> double { return W[n]; };
-      auto rnd = [&](int q) -> uint64_t {
-        return hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)q);
-      };
       auto out = [&](int q, int n) { idx[q] = n; };
       auto all = [](int) { return true; };
       lds_barrier();
       categorical_block<NT>(N, lmax, logit, B, all, rnd, out, cp128, red);
+      lds_barrier();  // idx for the trajectory tail
     } else {
-      // ---- backward-kernel rows (:400-435), one per distinct next state
-      if (B <= 64) {
-        if (wave_id() == 0) {
-          serial_begin();
-          const int lane = lane_id();
-          int g = -1;
-          if (lane < B) {
-            const uint64_t xb = X[lane];
-            g = lane;
-            for (int q = 0; q < lane; ++q)
-              if (X[q] == xb) { g = q; break; }
+      // ---- backward-kernel rows (:400-435), one per distinct next state.
+      // B <= 64: the groups (distinct next states, in order of first
+      // occurrence) were formed by wave 0 at the end of step t+1.
+      if (B > 64) {
+        if (tid == 0) {
+          int ng = 0;
+          for (int b = 0; b < B; ++b) {
+            int g = 0;
+            while (g < ng && gst[g] != X[b]) ++g;
+            if (g == ng) gst[ng++] = X[b];
+            grp[b] = g;
           }
-          const unsigned long long lead = __ballot(lane < B && g == lane);
-          if (lane < B) {
-            const int gi = __popcll(lead & ((1ull << g) - 1ull));  // leaders before this group's leader
-            grp[lane] = gi;
-            if (g == lane) gst[gi] = X[lane];
-          }
-          if (lane == 0) sh.ng = __popcll(lead);
-          serial_end();
+          sh.ng = ng;
         }
-      } else if (tid == 0) {
-        int ng = 0;
-        for (int b = 0; b < B; ++b) {
-          int g = 0;
-          while (g < ng && gst[g] != X[b]) ++g;
-          if (g == ng) gst[ng++] = X[b];
-          grp[b] = g;
-        }
-        sh.ng = ng;
+        lds_barrier();
       }
-      lds_barrier();
       const int ng = sh.ng;
       if (dbg && tid == 0) ph_acc[10] += ng;
       BPH(2);
-      bool fail = false;
       for (int g = 0; g < ng; ++g) {
         const uint64_t xn = gst[g];
         const int mn = hyg_st_m(xn), dcn = hyg_st_dc(xn), rcn = hyg_st_rc(xn), dkn = hyg_st_dk(xn),
                   rkn = hyg_st_rk(xn);
-        // ---- finite logits l_n = log f(xn | x_n) + W_n, gathered into a short
-        //      list (n, l_n): only a few dozen of the N candidates can reach xn
-        // Only slots whose child can have d_c = dcn - 1 (or a control change
-        // point when dcn = 1) can reach xn: lc of tg_trans is a constant -inf
-        // otherwise (ancestors always have d_c >= 1).
-        int r0a, r0b, r1a, r1b;
-        if (dcn >= 3) { r0a = 0; r0b = 1; r1a = K; r1b = 2 * K; }                         // A, C, D
-        else if (dcn == 2) { r0a = 1; r0b = K; r1a = 2 * K + rcn * K; r1b = r1a + K; }   // B, E(i = rcn)
-        else { r0a = 0; r0b = I; r1a = I; r1b = I; }
-        const int nseg0 = r0b - r0a, nseg = nseg0 + (r1b - r1a);
-        // Segment list (at most kSeg reachable slots): slot v's finite logits
-        // at [64 v, 64 v + c_v) in lane order, so the list is in n order by
-        // construction: no shared counter, no atomics, no rank sort
+        bool one_wave = false;
+        int L = 0, seg_incl = 0, nseg = 0;
         constexpr int kSeg = 16;
-        const bool segp = fast && nseg <= kSeg && Nmax >= 64 * kSeg + 160 && 4 * (NT + 1) >= 64 * kSeg;
-        if (!segp) {
-          if (tid == 0) sh.cnt = 0;
-          lds_barrier();  // (the segment path: every reader of the areas is behind the last group's barrier)
-        }
+        bool segp = false;
         int* lst_n = (int*)cp128;  // list indices (cp area, NT+1 u128 = 4(NT+1) ints)
-        double* lst_l = Lg;        // list logits
-        const int cap = (4 * (NT + 1) < Nmax) ? 4 * (NT + 1) : Nmax;
-        if (!fast) {
-          for (int n = tid; n < N; n += NT) {
-            const double w = W[n];
-            double l = HYG_NINF;
-            if (w > HYG_NINF) {
-              const double f = tg_trans(cl, K, state_of(n), xn, hz_of_n(n));
-              if (hyg_isfinite(f)) l = f + w;
-            }
-            if (l > HYG_NINF) {
-              const int pos = atomicAdd(&sh.cnt, 1);
-              if (pos < cap) { lst_n[pos] = n; lst_l[pos] = l; }
-            }
+        double* lst_l = Lg;        // list logits (the W area: W is not built on the list path)
+        if (fast) {
+          // ---- finite logits l_n = log f(xn | x_n) + W_n, gathered into a short
+          //      list (n, l_n): only a few dozen of the N candidates can reach xn.
+          // Only slots whose child can have d_c = dcn - 1 (or a control change
+          // point when dcn = 1) can reach xn: lc of tg_trans is a constant -inf
+          // otherwise (ancestors always have d_c >= 1).
+          int r0a, r0b, r1a, r1b;
+          if (dcn >= 3) { r0a = 0; r0b = 1; r1a = K; r1b = 2 * K; }                         // A, C, D
+          else if (dcn == 2) { r0a = 1; r0b = K; r1a = 2 * K + rcn * K; r1b = r1a + K; }   // B, E(i = rcn)
+          else { r0a = 0; r0b = I; r1a = I; r1b = I; }
+          const int nseg0 = r0b - r0a;
+          nseg = nseg0 + (r1b - r1a);
+          // Segment list (at most kSeg reachable slots): slot v's finite logits
+          // at [64 v, 64 v + c_v) in lane order, so the list is in n order by
+          // construction: no shared counter, no atomics, no rank sort
+          segp = nseg <= kSeg && Nmax >= 64 * kSeg + 160 && 4 * (NT + 1) >= 64 * kSeg;
+          if (!segp) {
+            if (tid == 0) sh.cnt = 0;
+            lds_barrier();  // (the segment path: every reader of the areas is behind the last group's barrier)
           }
-        } else {
+          const int cap = (4 * (NT + 1) < Nmax) ? 4 * (NT + 1) : Nmax;
           constexpr int NW = NT / 64;
           const int lane = lane_id(), wv = wave_id();
           const bool act = lane < np;
@@ -2023,7 +2009,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
               }
               double l = HYG_NINF;
               if (poss) {
-                const double w = weight_at(cl, K, lane, sl, s.mode, s.log_c, s.lse, P, pw, PHZ, Et);
+                const double w = weight_at(cl, K, lane, sl, s.mode, s.log_c, s.lse, P, PW, PHZ, Et);
                 if (w > HYG_NINF) {
                   const double f = tg_trans_sel(cl.lPm[x.m * 2 + mn], cl.lPc[x.rc * K + rcn], cl.lU1, cl.lU2,
                                                 cl.u, x.m, x.dc, x.rc, x.dk, x.rk, xn, x.h);
@@ -2050,20 +2036,18 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
               }
             }
           }
+          lds_barrier();
+          BPH(3);
+          // segment path: inclusive prefix of the segment counts in every wave
+          seg_incl = segp ? wave_incl_int(lane_id() < nseg ? sh.segc[lane_id()] : 0) : 0;
+          L = segp ? __builtin_amdgcn_readlane(seg_incl, 63) : sh.cnt;
+          if (dbg && tid == 0) ph_acc[11] += L;
+          if (L == 0) { fail = true; break; }  // uniform: every logit -inf
+          one_wave = L <= 64 && Nmax >= 192;
         }
-        lds_barrier();
-        BPH(3);
-        // segment path: inclusive prefix of the segment counts in every wave
-        const int seg_incl = segp ? wave_incl_int(lane_id() < nseg ? sh.segc[lane_id()] : 0) : 0;
-        const int L = segp ? __builtin_amdgcn_readlane(seg_incl, 63) : sh.cnt;
-        if (dbg && tid == 0) ph_acc[11] += L;
-        if (L == 0) { fail = true; break; }  // uniform: every logit -inf
-        auto rnd = [&](int b) -> uint64_t {
-          return hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_BACKWARD, (uint64_t)t, (uint64_t)b);
-        };
         if (pre_bits && g == 0 && t >= 1 && wave_id() == NT / 64 - 1)  // next step's bits, while wave 0 draws
           backward_bits(rb + ((t - 1) & 1) * rbs, B, t - 1, ch.seed, ch.chain_id);
-        if (L <= 64 && B <= 64 && Nmax >= 192) {
+        if (one_wave) {
           // ---- one wave: order the list by n, exact masses, scan, draws
           if (wave_id() == 0) {
             serial_begin();
@@ -2123,10 +2107,12 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             serial_end();
           }
           BPH(4);
+          if (g + 1 < ng) lds_barrier();  // the next group's list reuses the areas wave 0 read
         } else {
-          // ---- general case: logits of all N in index order, block categorical
+          // ---- general case: logits of all N in index order (built in place of
+          //      the weights), block categorical
           if (!w_ready) {
-            lds_barrier();  // the list areas are reused below
+            lds_barrier();  // the list areas (= the W area) are reused below
             make_W();
             lds_barrier();
           }
@@ -2138,61 +2124,108 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
               const double f = tg_trans(cl, K, state_of(n), xn, hz_of_n(n));
               if (hyg_isfinite(f)) l = f + w;
             }
-            Lg[n] = l;
+            W[n] = l;  // each n read and rewritten by one thread
             m = dmax(m, l);
           }
+          w_ready = false;  // W holds this group's logits now
           const double lmax = block_max<NT>(m, red);
-          auto logit = [&](int n) -> double { return Lg[n]; };
+          if (!(lmax > HYG_NINF)) { fail = true; break; }  // uniform: every logit -inf
+          auto logit = [&](int n) -> double { return W[n]; };
           auto in_g = [&](int b) { return grp[b] == g; };
           auto out = [&](int b, int n) { idx[b] = n; };
           categorical_block<NT>(N, lmax, logit, B, in_g, rnd, out, cp128, red);
+          lds_barrier();
         }
-        lds_barrier();
         BPH(5);
       }
       if (fail) { if (tid == 0) sh.status = HYG_ENUMERIC; lds_barrier(); break; }
     }
-    lds_barrier();
     // ---- trajectories and test-function means at t (run_inference_two_groups.py:233-240, 294-314)
-    if (B <= 64 && wave_id() == 0) serial_begin();  // (ended after the means)
-    for (int b = tid; b < B; b += NT) {
-      const uint64_t x = state_of(idx[b]);
-      X[b] = x;
-      const size_t o = (size_t)(ch.out_begin + t) * B + b;
-      o_merged[o] = (int16_t)hyg_st_m(x);
-      o_control[2 * o + 0] = (int16_t)hyg_st_dc(x);
-      o_control[2 * o + 1] = (int16_t)hyg_st_rc(x);
-      o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
-      o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
-    }
-    if (B <= 64 && wave_id() == 0) {  // trajectory b on lane b of wave 0 (its own X write): means by ballots
-      serial_begin();
-      const int lane = lane_id();
-      const bool v = lane < B;
-      const uint64_t x = v ? X[lane] : 0ull;
-      int myc = __builtin_popcountll(__ballot(v && hyg_st_m(x) == 0));
-      for (int r = 0; r < K; ++r) {
-        const int cc = __builtin_popcountll(__ballot(v && hyg_st_rc(x) == r));
-        const int ck = __builtin_popcountll(__ballot(v && hyg_st_rk(x) == r));
-        myc = (lane == 1 + r) ? cc : ((lane == 1 + K + r) ? ck : myc);
+    if (B <= 64) {
+      // wave 0 alone: trajectory b on lane b (idx written by this wave's draws,
+      // or behind a barrier), then the groups of step t-1's next states
+      if (wave_id() == 0) {
+        serial_begin();
+        wave_lds_sync();
+        const int lane = lane_id();
+        const bool v = lane < B;
+        uint64_t x = 0;
+        if (v) {
+          x = state_of(idx[lane]);
+          const size_t o = (size_t)(ch.out_begin + t) * B + lane;
+          o_merged[o] = (int16_t)hyg_st_m(x);
+          o_control[2 * o + 0] = (int16_t)hyg_st_dc(x);
+          o_control[2 * o + 1] = (int16_t)hyg_st_rc(x);
+          o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
+          o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
+        }
+        int myc = __builtin_popcountll(__ballot(v && hyg_st_m(x) == 0));
+        for (int r = 0; r < K; ++r) {
+          const int cc = __builtin_popcountll(__ballot(v && hyg_st_rc(x) == r));
+          const int ck = __builtin_popcountll(__ballot(v && hyg_st_rk(x) == r));
+          myc = (lane == 1 + r) ? cc : ((lane == 1 + K + r) ? ck : myc);
+        }
+        if (lane < 2 * K + 1) {
+          const float vv = (float)myc / (float)B;
+          if (lane == 0) o_split[ch.out_begin + t] = vv;
+          else o_regime[(size_t)(ch.out_begin + t) * K2 + (lane - 1)] = vv;
+        }
+        BPH(6);
+        if (t > 0) {
+          // distinct states in order of first occurrence, by ballots: one
+          // iteration per group (about one per step)
+          uint64_t rem = __ballot(v);
+          int gi = 0, mg = 0;
+          while (rem) {  // uniform
+            const int ld = (int)__builtin_ctzll(rem);
+            const uint64_t xv = rdlane64(x, ld);
+            const uint64_t eq = __ballot(v && x == xv);
+            if (lane == 0) gst[gi] = xv;
+            mg = ((eq >> lane) & 1) ? gi : mg;
+            rem &= ~eq;
+            ++gi;
+          }
+          if (v) grp[lane] = mg;
+          if (lane == 0) sh.ng = gi;
+        }
+        serial_end();
       }
-      if (lane < 2 * K + 1) {
-        const float vv = (float)myc / (float)B;
-        if (lane == 0) o_split[ch.out_begin + t] = vv;
-        else o_regime[(size_t)(ch.out_begin + t) * K2 + (lane - 1)] = vv;
+    } else {
+      for (int b = tid; b < B; b += NT) {
+        const uint64_t x = state_of(idx[b]);
+        X[b] = x;
+        const size_t o = (size_t)(ch.out_begin + t) * B + b;
+        o_merged[o] = (int16_t)hyg_st_m(x);
+        o_control[2 * o + 0] = (int16_t)hyg_st_dc(x);
+        o_control[2 * o + 1] = (int16_t)hyg_st_rc(x);
+        o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
+        o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
       }
-      serial_end();
+      lds_barrier();
+      if (tid < 2 * K + 1) {
+        int cntv = 0;
+        for (int b = 0; b < B; ++b) {
+          const uint64_t x = X[b];
+          if (tid == 0) cntv += (hyg_st_m(x) == 0);
+          else if (tid <= K) cntv += (hyg_st_rc(x) == tid - 1);
+          else cntv += (hyg_st_rk(x) == tid - 1 - K);
+        }
+        const float v = (float)cntv / (float)B;
+        if (tid == 0) o_split[ch.out_begin + t] = v;
+        else o_regime[(size_t)(ch.out_begin + t) * K2 + (tid - 1)] = v;
+      }
     }
-    BPH(6);
-    // ---- record t-1 (+ hazard rows) replaces record t once every read of it is done
-    lds_barrier();
+    // ---- record t-1 (+ hazard rows) into the other buffer: its last readers
+    //      (step t+1) are behind this step's barriers; the emission block into
+    //      the ring half whose rows this step no longer reads
     if (have1) {
-      pst[tid] = st1;
-      pw[tid] = w1;
+      const int o = (bt ^ 1) * M + tid;
+      pst[o] = st1;
+      pw[o] = w1;
       Hz4 h;
       h.lrc = h1c.x; h.l1c = h1c.y; h.lrk = h1k.x; h.l1k = h1k.y;
-      phz[tid] = h;
-      pf[tid] = pf1;
+      phz[o] = h;
+      pf[o] = pf1;
     }
     if (eload) {
       double* dst = ering + (size_t)((t / kEBlock - 2) & 1) * kEBlock * K2;
@@ -2203,18 +2236,6 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       }
     }
     lds_barrier();
-    if (B > 64 && tid < 2 * K + 1) {
-      int cntv = 0;
-      for (int b = 0; b < B; ++b) {
-        const uint64_t x = X[b];
-        if (tid == 0) cntv += (hyg_st_m(x) == 0);
-        else if (tid <= K) cntv += (hyg_st_rc(x) == tid - 1);
-        else cntv += (hyg_st_rk(x) == tid - 1 - K);
-      }
-      const float v = (float)cntv / (float)B;
-      if (tid == 0) o_split[ch.out_begin + t] = v;
-      else o_regime[(size_t)(ch.out_begin + t) * K2 + (tid - 1)] = v;
-    }
     s = s1;
     st1 = st2;
     w1 = w2;
@@ -2467,7 +2488,7 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
     for (int i = 0; i < n_chains; ++i)
       for (int k = 0; k < kPh; ++k) tot[k] += h[(size_t)i * kPh + k];
     const double steps = (double)tot[kPh - 1];
-    const char* nm[7] = {"gen", "issue", "dedupe", "list", "wave0", "tail", "traj"};
+    const char* nm[7] = {"copy+gen", "issue", "groups", "list", "wave0", "general", "traj"};
     fprintf(stderr, "[hyg backward phases NT=%d] cycles/step:", NT);
     double sum = 0;
     for (int k = 0; k < 7; ++k) {
