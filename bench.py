@@ -396,7 +396,8 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": workload, "chains_per_rank": len(chains), "launches_per_step": len(runs),
-                   "threads_per_chain": int(L.hyg_tg_threads_per_chain(model.handle, len(chains))),
+                   "threads_per_chain": int(L.hyg_tg_threads_per_chain(model.handle, len(batches[0]))),
+                   "chains_per_cu_resident": int(L.hyg_tg_chains_per_cu(model.handle, len(batches[0]))),
                    "global_sites_x_seeds": total_units,
                    "parallelism": f"chains over {world} rank(s) on {n_gpus} GPU(s)"},
         "roofline": roof,

@@ -299,6 +299,11 @@ int32_t hyg_tg_threads_per_chain(const hyg_tg_model* m, int32_t n_chains) {
   return m ? hyg::tg_threads_per_chain(m->c, n_chains) : 0;
 }
 
+int32_t hyg_tg_chains_per_cu(const hyg_tg_model* m, int32_t n_chains) {
+  if (!m || !m->on_device) return 0;
+  return hyg::tg_resident_per_cu(m->c, n_chains);
+}
+
 int hyg_tg_force_threads(int32_t forward, int32_t backward) {
   const int rc = hyg::tg_force_threads(forward, backward);
   return rc == HYG_OK ? rc : fail(rc, "unsupported workgroup size");

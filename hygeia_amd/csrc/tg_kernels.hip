@@ -356,18 +356,22 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
     l.bpos = o + sizeof(int) * kBuckets;
     l.bcnt_bytes = bb;
     o = align_up(o + bb, 16);
-    l.pre64 = o; o = align_up(o + sizeof(hyg_u192) * (M < 64 ? M : 64), 16);
+    // the fallback's prefix of the first min(M, 64) sorted positions: written
+    // after the counting sort's last use of the bucket area, last read before
+    // the systematic thresholds are written there (a barrier apart)
+    l.pre64 = l.bcnt;
     // per-wave partials of the top-set resampling path (counts per cutoff, mass)
     l.part = o; o = align_up(o + (sizeof(int) * kNCut + sizeof(hyg_u192)) * (NT / 64), 16);
   }
-  // the ancestors of the current step: one buffer in the forward (rewritten
-  // behind a barrier), two in the backward (record t in buffer t & 1 while
-  // record t-1 is stored into the other)
-  const size_t nb = backward ? 2 : 1;
-  l.pst = o; o = align_up(o + sizeof(uint64_t) * M * nb, 16);
-  l.pw = o; o = align_up(o + sizeof(double) * M * nb, 16);
-  l.phz = o; o = align_up(o + sizeof(Hz4) * M * nb, 16);
-  l.pf = o; o = align_up(o + sizeof(Pf3) * M * nb, 16);
+  // the ancestors of the current step, two buffers: the forward gathers the
+  // next step's ancestors into the other buffer while this step's are read;
+  // the backward holds record t in buffer t & 1 while record t-1 is stored
+  // into the other. (The forward's hazard-row prefetch pf is written after
+  // the weights, which do not read it: one buffer.)
+  l.pst = o; o = align_up(o + sizeof(uint64_t) * M * 2, 16);
+  l.pw = o; o = align_up(o + sizeof(double) * M * 2, 16);
+  l.phz = o; o = align_up(o + sizeof(Hz4) * M * 2, 16);
+  l.pf = o; o = align_up(o + sizeof(Pf3) * M * (backward ? 2 : 1), 16);
   l.ering = o; o = align_up(o + sizeof(double) * 2 * kEBlock * 2 * K, 16);
   l.cl = o; o = align_up(o + const_lds_bytes(K), 16);
   l.parents = o; o = align_up(o + sizeof(int) * (M > B ? M : B), 16);
@@ -1331,9 +1335,10 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
   int* bpos = (int*)(smem + lay.bpos);
   hyg_u192* tau = (hyg_u192*)(smem + lay.bcnt);
   hyg_u192* pre64 = (hyg_u192*)(smem + lay.pre64);
-  uint64_t* pst = (uint64_t*)(smem + lay.pst);
-  double* pw = (double*)(smem + lay.pw);
-  Hz4* phz = (Hz4*)(smem + lay.phz);
+  uint64_t* pst0 = (uint64_t*)(smem + lay.pst);  // [2][M]: buffer `cur` holds the current ancestors
+  double* pw0 = (double*)(smem + lay.pw);
+  Hz4* phz0 = (Hz4*)(smem + lay.phz);
+  int cur = 0;
   Pf3* pf = (Pf3*)(smem + lay.pf);
   double* ering = (double*)(smem + lay.ering);
   ConstLds& cl = *(ConstLds*)(smem + lay.cl);
@@ -1381,6 +1386,10 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
 
   if (dbg && tid == 0) ph_acc[kPh - 1] = __builtin_amdgcn_s_memtime();
   for (int t = 1; t < T; ++t) {
+    // the ancestors of step t-1's particles (read by the regenerations and the gather)
+    const uint64_t* pst = pst0 + cur * M;
+    const double* pw = pw0 + cur * M;
+    const Hz4* phz = phz0 + cur * M;
     // emission rows one block ahead: issue at the block start, land in the ring later
     const bool eload = ((t % kEBlock) == 0) && (t + kEBlock < T);
     PH(0);
@@ -1482,6 +1491,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     PH(1);
     int mode, np;
     float log_c = 0.0f;
+    bool need_bar = true;  // parents written by many threads, no barrier behind them yet
     if (cnt <= M) {
       // ---- keep every particle with non-zero weight, in index order (:207-209)
       mode = MODE_KEEP;
@@ -1555,9 +1565,11 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         categorical_block<NT>(N, lmax, logit, M, all, rnd, out, cp128, red);
       } else {
         mode = MODE_OPTIMAL;
+        // the top-set path's parents (wave 0) and sh.* are behind its last barrier
+        need_bar = fs != FAST_DONE;
       }
     }
-    lds_barrier();
+    if (need_bar) lds_barrier();
     PH(4);
     // (np <= M <= 64 at the pipeline shape: the gather is wave 0's alone)
     if (wave_id() == 0) serial_begin();
@@ -1642,16 +1654,19 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     prev_mode = mode;
     prev_logc = log_c;
     prev_lse = lse;
-    lds_barrier();  // every read of the previous ancestors is done
+    // the new ancestors into the other buffer: its last readers (step t-1's
+    // weights) are behind this step's barriers
     if (have_pf) {
-      pst[tid] = gs;
-      pw[tid] = gw;
-      phz[tid] = gh;
+      const int o = (cur ^ 1) * M + tid;
+      pst0[o] = gs;
+      pw0[o] = gw;
+      phz0[o] = gh;
     }
     lds_barrier();
+    cur ^= 1;
     PH(5);
     // ---- propose and weight the particles of step t
-    gen_weights<NT>(cl, K, I, np, mode, log_c, lse, pst, pw, phz,
+    gen_weights<NT>(cl, K, I, np, mode, log_c, lse, pst0 + cur * M, pw0 + cur * M, phz0 + cur * M,
                     erow(ering, t, K2), W, &mloc, &cloc);
     PH(7);
     N = I * np;
@@ -2499,6 +2514,26 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
             (double)(tot[11] & 0xffffffffull) / (tot[10] > 0 ? (double)tot[10] : 1.0));
   }
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
+}
+
+// Forward workgroups one CU holds at the width a launch of n_chains uses
+// (the occupancy query on the kernel instantiation and its dynamic LDS).
+template <int NT>
+static int fwd_resident_nt(const hyg_tg_consts& c) {
+  const Lay lf = make_layout(c.K, c.M, c.B, c.Nmax, NT, false);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fwd_kernel<NT>(c), NT, lf.total) != hipSuccess)
+    return -1;
+  return nb;
+}
+int tg_resident_per_cu(const hyg_tg_consts& c, int n_chains) {
+  switch (threads_per_chain(false, c, n_chains)) {
+    case 64: return fwd_resident_nt<64>(c);
+    case 128: return fwd_resident_nt<128>(c);
+    case 256: return fwd_resident_nt<256>(c);
+    case 768: return fwd_resident_nt<768>(c);
+    default: return fwd_resident_nt<512>(c);
+  }
 }
 
 int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,

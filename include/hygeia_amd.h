@@ -115,6 +115,12 @@ int32_t hyg_tg_num_particles(const hyg_tg_model* model);
  * runs one chain per CPU process, modules/two_group/4_infer.nf:28). */
 int32_t hyg_tg_threads_per_chain(const hyg_tg_model* model, int32_t n_chains);
 
+/* Forward-kernel workgroups (chains) one CU holds at the width a launch of
+ * n_chains uses (the HIP occupancy query with the kernel's LDS): 3 for the
+ * pipeline shape at 256 threads, 1 at the low-occupancy width. 0 without a
+ * device. Diagnostic. */
+int32_t hyg_tg_chains_per_cu(const hyg_tg_model* model, int32_t n_chains);
+
 /* Test / tuning override of the chain workgroup sizes for every later launch
  * in the process: forward and backward threads (64, 128, 256, 512 or 768;
  * 0 = the automatic choice above). Not thread-safe. The results do not depend

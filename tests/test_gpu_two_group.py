@@ -141,6 +141,9 @@ def test_width_selection_by_chains_per_cu():
     mu, sg = syn.regime_params(6)
     m6 = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(6), max_total_reads=200, max_duration=100)
     assert [L.hyg_tg_threads_per_chain(m6.handle, n) for n in (1, cus, cus + 1, 582)] == [512, 512, 256, 256]
+    # the C3 shape keeps three chains per CU at 256 threads (LDS <= 160 KiB / 3)
+    assert L.hyg_tg_chains_per_cu(m6.handle, 582) == 3
+    assert L.hyg_tg_chains_per_cu(m6.handle, 73) >= 1
     mu, sg = syn.regime_params(12)
     m12 = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(12), max_total_reads=200, max_duration=100)
     assert L.hyg_tg_threads_per_chain(m12.handle, 10) == 512
