@@ -2403,8 +2403,8 @@ FwdFn fwd_kernel(const hyg_tg_consts& c) {
   }
   if constexpr (NT == 256 || NT == 512 || NT == 768)
     if (shape_specialised(c)) return &tg_forward_kernel<NT, 6, 50, 25>;
-  if constexpr (NT == 512)
-    if (shape_c5(c)) return &tg_forward_kernel<512, 12, 50, 25>;
+  if constexpr (NT == 512 || NT == 768)
+    if (shape_c5(c)) return &tg_forward_kernel<NT, 12, 50, 25>;
   return &tg_forward_kernel<NT>;
 }
 template <int NT>
@@ -2417,8 +2417,8 @@ BwdFn bwd_kernel(const hyg_tg_consts& c) {
   }
   if constexpr (NT == 256 || NT == 512 || NT == 768)
     if (shape_specialised(c)) return &tg_backward_kernel<NT, 6, 50, 25>;
-  if constexpr (NT == 512)
-    if (shape_c5(c)) return &tg_backward_kernel<512, 12, 50, 25>;
+  if constexpr (NT == 512 || NT == 768)
+    if (shape_c5(c)) return &tg_backward_kernel<NT, 12, 50, 25>;
   return &tg_backward_kernel<NT>;
 }
 
