@@ -1151,7 +1151,6 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
 // candidate lists before the log-sum-exp reduction.
 template <int NT, int NSW>
 __device__ __forceinline__ int top_set_resample(const double* W, int N, double mx, double logS, const int* lst, int lb, int cw,
-                                int cap, int cw2,
                                 unsigned char* scr, size_t scr_bytes, uint64_t* srt, size_t srt_bytes,
                                 const int* part_cnt, hyg_u192* part_tot, int* parents, Shared& sh,
                                 const ConstLds& cl, unsigned char* red, int M, int cnt_fin, float Usys,
@@ -1186,52 +1185,48 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
   // ---- 2. gather A's keys; exact mass of the list weights outside A. From the
   // third cutoff on (X >= 20 nats below the top: every outside mass is below
   // e^-20 < 2^-28.8, its image m 2^149 below 2^120.2, and a lane sums at most
-  // ceil(N / NT) + 2 <= 128 of them (two lists), below 2^127.2) a lane's
-  // images are formed and summed as u128.
-  const bool narrow = ks >= kNarrowCut && (N + NT - 1) / NT + 2 <= kNarrowPerLane;
+  // ceil(N / NT) <= 128 of them, below 2^127.2) a lane's images are formed and
+  // summed as u128.
+  const bool narrow = ks >= kNarrowCut && (N + NT - 1) / NT <= kNarrowPerLane;
   hyg_u192 mb = hyg_u192_zero(), mb2 = hyg_u192_zero();
   hyg_u128 nb = hyg_u128_zero(), nb2 = hyg_u128_zero();
   constexpr int kLR = kLRof<NT>;
-  // the wave's L1 (front of its region) and L2 (back) entries
-  for (int seg = 0; seg < 2; ++seg) {
-    const int s0 = seg ? lb + cap - cw2 : lb, sc = seg ? cw2 : cw;
-    for (int b = 0; b < sc; b += 64 * kLR) {  // kLR entries per lane, loads first (see the lse loop)
-      int nn[kLR];
-      float lw[kLR];
-      bool inA[kLR], outA[kLR];
+  for (int b = 0; b < cw; b += 64 * kLR) {  // kLR entries per lane, loads first (see the lse loop)
+    int nn[kLR];
+    float lw[kLR];
+    bool inA[kLR], outA[kLR];
+#pragma unroll
+    for (int r = 0; r < kLR; ++r) {
+      const int i = b + r * 64 + lane;
+      nn[r] = lst[lb + (i < cw ? i : b)];
+    }
+#pragma unroll
+    for (int r = 0; r < kLR; ++r) {
+      const bool v = b + r * 64 + lane < cw;
+      const double x = W[nn[r]] - mx;
+      lw[r] = (float)(x - logS);
+      inA[r] = v && x >= cutx;
+      outA[r] = v && !inA[r];
+    }
+#pragma unroll
+    for (int r = 0; r < kLR; ++r) {
+      const uint64_t bal = wave_ballot(inA[r]);
+      if (inA[r]) srt[off + lanes_below(bal)] = sort_key(lw[r], nn[r]);
+      off += (int)__builtin_popcountll(bal);
+    }
+    if (hasB && narrow) {  // uniform; expf(lw) is 0 below sig_thresh
 #pragma unroll
       for (int r = 0; r < kLR; ++r) {
-        const int i = b + r * 64 + lane;
-        nn[r] = lst[s0 + (i < sc ? i : b)];
+        const float m = hyg_expf(lw[r]);
+        const hyg_u128 f = hyg_fix149f_low128(outA[r] ? m : 0.0f);
+        if (r & 1) nb2 = hyg_u128_add(nb2, f); else nb = hyg_u128_add(nb, f);
       }
+    } else if (hasB) {
 #pragma unroll
       for (int r = 0; r < kLR; ++r) {
-        const bool v = b + r * 64 + lane < sc;
-        const double x = W[nn[r]] - mx;
-        lw[r] = (float)(x - logS);
-        inA[r] = v && x >= cutx;
-        outA[r] = v && !inA[r];
-      }
-#pragma unroll
-      for (int r = 0; r < kLR; ++r) {
-        const uint64_t bal = wave_ballot(inA[r]);
-        if (inA[r]) srt[off + lanes_below(bal)] = sort_key(lw[r], nn[r]);
-        off += (int)__builtin_popcountll(bal);
-      }
-      if (hasB && narrow) {  // uniform; expf(lw) is 0 below sig_thresh
-#pragma unroll
-        for (int r = 0; r < kLR; ++r) {
-          const float m = hyg_expf(lw[r]);
-          const hyg_u128 f = hyg_fix149f_low128(outA[r] ? m : 0.0f);
-          if (r & 1) nb2 = hyg_u128_add(nb2, f); else nb = hyg_u128_add(nb, f);
-        }
-      } else if (hasB) {
-#pragma unroll
-        for (int r = 0; r < kLR; ++r) {
-          const float m = hyg_expf(lw[r]);
-          const hyg_u192 f = hyg_fix149f(outA[r] ? m : 0.0f);
-          if (r & 1) mb2 = hyg_u192_add(mb2, f); else mb = hyg_u192_add(mb, f);
-        }
+        const float m = hyg_expf(lw[r]);
+        const hyg_u192 f = hyg_fix149f(outA[r] ? m : 0.0f);
+        if (r & 1) mb2 = hyg_u192_add(mb2, f); else mb = hyg_u192_add(mb, f);
       }
     }
   }
@@ -1407,15 +1402,9 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     // ---- per wave, the list of candidates with W - mx >= sig_thresh (keys
     //      area): every nonzero F=100 mass (x >= -70) and every significant
     //      f32 log-weight is on it; candidates interleaved over the waves
-    // Two lists in one per-wave region of lst_cap entries: L1 (x = W - mx >=
-    // -70, every nonzero F = 100 mass) from the front, L2 (sig_thresh <= x <
-    // -70: significant f32 log-weights whose F = 100 mass is 0) from the back.
-    // The log-sum-exp runs over L1 only; the top set and its outside masses
-    // take both.
     int* lst = (int*)keys;
-    const int lst_cap = ((N + NT - 1) / NT) * 64;
-    const int lst_base = wave_id() * lst_cap;
-    int lst_cnt = 0, lst_cnt2 = 0;
+    const int lst_base = wave_id() * (((N + NT - 1) / NT) * 64);
+    int lst_cnt = 0;
     const bool topset = cnt > M && M <= 64;  // this step resamples by the top-set path
     {
       // kCC candidates per lane at a time, their loads issued together (a
@@ -1424,25 +1413,20 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       // (the shape-specialised kernel: every candidate in one pass, N <= M I)
       constexpr int kCC = KC ? (MC * (2 * KC + KC * KC) + NT - 1) / NT : 8;
       for (int b0 = wave_id() * 64; b0 < N; b0 += kCC * NT) {
-        bool keep1[kCC], keep2[kCC];
+        bool keep[kCC];
 #pragma unroll
         for (int j = 0; j < kCC; ++j) {
           const int n = b0 + j * NT + lane_id();
           const double w = W[n < N ? n : 0];
           // `&`, not `&&`: a short-circuit test puts the load under a branch
           // and waits out its round trip before the next candidate's load
-          const double x = w - mx;
-          keep1[j] = (n < N) & (x >= -70.0);
-          keep2[j] = (n < N) & (x >= cutw) & !(x >= -70.0);
+          keep[j] = (n < N) & (w - mx >= cutw);
         }
 #pragma unroll
         for (int j = 0; j < kCC; ++j) {
-          const uint64_t bal = wave_ballot(keep1[j]);
-          const uint64_t bal2 = wave_ballot(keep2[j]);
-          if (keep1[j]) lst[lst_base + lst_cnt + lanes_below(bal)] = b0 + j * NT + lane_id();
-          if (keep2[j]) lst[lst_base + lst_cap - 1 - (lst_cnt2 + lanes_below(bal2))] = b0 + j * NT + lane_id();
+          const uint64_t bal = wave_ballot(keep[j]);
+          if (keep[j]) lst[lst_base + lst_cnt + lanes_below(bal)] = b0 + j * NT + lane_id();
           lst_cnt += (int)__builtin_popcountll(bal);
-          lst_cnt2 += (int)__builtin_popcountll(bal2);
         }
       }
       wave_lds_sync();
@@ -1492,7 +1476,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         if (lane_id() == 0) {  // read after the reduction's barriers below
 #pragma unroll
           for (int k = 0; k < kNCut - 1; ++k) part_cnt[wave_id() * kNCut + k] = ccut[k];
-          part_cnt[wave_id() * kNCut + kNCut - 1] = lst_cnt + lst_cnt2;
+          part_cnt[wave_id() * kNCut + kNCut - 1] = lst_cnt;
         }
       }
       const hyg_u128 sacc = hyg_u128_add(s0, s1);
@@ -1531,8 +1515,7 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       PH(2);
       int fs = FAST_FALLBACK;
       if (topset)
-        fs = top_set_resample<NT, kSortWaves<NT>>(W, N, mx, logS, lst, lst_base, lst_cnt, lst_cap, lst_cnt2,
-                                                  smem + lay.W, lay.bcnt - lay.W,
+        fs = top_set_resample<NT, kSortWaves<NT>>(W, N, mx, logS, lst, lst_base, lst_cnt, smem + lay.W, lay.bcnt - lay.W,
                                   (uint64_t*)(smem + lay.bcnt), lay.bcnt_bytes, part_cnt, part_tot, parents, sh, cl,
                                   red, M, cnt, Ucur, lay.topset_r, ph_acc, dbg != nullptr);
       PH(20);
