@@ -89,8 +89,7 @@ __device__ __forceinline__ void exp_fix100_lockstep(const double (&x)[R], hyg_u1
   for (int i = 0; i < R; ++i) {
     k[i] = (int)kd[i];
     const double hi = xc[i] - kd[i] * HYG_LN2_HI;
-    const double lo = kd[i] * HYG_LN2_LO;
-    r[i] = hi - lo;
+    r[i] = __builtin_fma(-kd[i], HYG_LN2_LO, hi);
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) r2[i] = r[i] * r[i];
@@ -99,20 +98,20 @@ __device__ __forceinline__ void exp_fix100_lockstep(const double (&x)[R], hyg_u1
 #pragma unroll
   for (int i = 0; i < R; ++i) r8[i] = r4[i] * r4[i];
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const double q0 = 1.0 + 1.0 * r[i];
-    const double q1 = 0.5 + 1.6666666666666665741e-01 * r[i];
-    const double q2 = 4.1666666666666664354e-02 + 8.3333333333333332177e-03 * r[i];
-    const double q3 = 1.3888888888888888889e-03 + 1.9841269841269841253e-04 * r[i];
-    const double q4 = 2.4801587301587301566e-05 + 2.7557319223985890653e-06 * r[i];
-    const double q5 = 2.7557319223985890653e-07 + 2.5052108385441718775e-08 * r[i];
-    const double q6 = 2.0876756987868098979e-09 + 1.6059043836821614599e-10 * r[i];
-    const double s0 = q0 + q1 * r2[i];
-    const double s1 = q2 + q3 * r2[i];
-    const double s2 = q4 + q5 * r2[i];
-    const double u0 = s0 + s1 * r4[i];
-    const double u1 = s2 + q6 * r4[i];
-    p[i] = u0 + u1 * r8[i];
+  for (int i = 0; i < R; ++i) {  // hyg__exp_poly, statement by statement
+    const double q0 = __builtin_fma(1.0, r[i], 1.0);
+    const double q1 = __builtin_fma(1.6666666666666665741e-01, r[i], 0.5);
+    const double q2 = __builtin_fma(8.3333333333333332177e-03, r[i], 4.1666666666666664354e-02);
+    const double q3 = __builtin_fma(1.9841269841269841253e-04, r[i], 1.3888888888888888889e-03);
+    const double q4 = __builtin_fma(2.7557319223985890653e-06, r[i], 2.4801587301587301566e-05);
+    const double q5 = __builtin_fma(2.5052108385441718775e-08, r[i], 2.7557319223985890653e-07);
+    const double q6 = __builtin_fma(1.6059043836821614599e-10, r[i], 2.0876756987868098979e-09);
+    const double s0 = __builtin_fma(q1, r2[i], q0);
+    const double s1 = __builtin_fma(q3, r2[i], q2);
+    const double s2 = __builtin_fma(q5, r2[i], q4);
+    const double u0 = __builtin_fma(s1, r4[i], s0);
+    const double u1 = __builtin_fma(q6, r4[i], s2);
+    p[i] = __builtin_fma(u1, r8[i], u0);
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) out[i] = hyg_exp_fix100_pk(p[i], k[i], x[i]);

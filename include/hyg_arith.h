@@ -7,10 +7,11 @@
  * HIP kernels alike, so that both produce bit-identical trajectories:
  *
  *   - hyg_exp / hyg_log: exp and log built from IEEE-754 basic operations only
- *     (+ - * / floor, no FMA: every translation unit is compiled with
- *     -ffp-contract=off). libm / ocml differ in the last ulp between host and
- *     device; these do not. Accuracy is ~1 ulp (tests/test_arith.py pins them
- *     against libm).
+ *     (+ - * / floor and EXPLICIT fused multiply-adds, fma() / v_fma_f64, which
+ *     IEEE 754 defines with one rounding, so host and device agree; no implicit
+ *     contraction: every translation unit is compiled with -ffp-contract=off).
+ *     libm / ocml differ in the last ulp between host and device; these do
+ *     not. Accuracy is ~1 ulp (tests/test_arith.py pins them against libm).
  *   - exact fixed-point mass sums. The reference sums exp(weights) with
  *     order-dependent float cumsums (resampling_functions.py:10,59; the TF
  *     multinomial CDF behind tfd.Categorical.sample,
@@ -42,6 +43,8 @@
 #define HYG_FMIN(a, b) __builtin_fmin(a, b)
 #define HYG_FMAX(a, b) __builtin_fmax(a, b)
 #define HYG_FLOORF(x) __builtin_floorf(x)
+#define HYG_FMA(a, b, c) __builtin_fma(a, b, c)
+#define HYG_FMAF(a, b, c) __builtin_fmaf(a, b, c)
 #define HYG_FMINF(a, b) __builtin_fminf(a, b)
 #define HYG_FMAXF(a, b) __builtin_fmaxf(a, b)
 #else
@@ -66,6 +69,10 @@ static inline float hyg__fmaxf(float a, float b) { return (a > b) ? a : ((a != a
 #define HYG_FMIN(a, b) hyg__fmin(a, b)
 #define HYG_FMAX(a, b) hyg__fmax(a, b)
 #define HYG_FLOORF(x) hyg__floorf(x)
+/* IEEE fused multiply-add (one rounding): C99 fma / fmaf, correctly rounded by
+ * definition (the oracle builds with -mfma: the x86 FMA3 instructions) */
+#define HYG_FMA(a, b, c) fma(a, b, c)
+#define HYG_FMAF(a, b, c) fmaf(a, b, c)
 #define HYG_FMINF(a, b) hyg__fminf(a, b)
 #define HYG_FMAXF(a, b) hyg__fmaxf(a, b)
 #endif
@@ -99,29 +106,33 @@ HYG_HD double hyg_pow2(int e) { return hyg_bits_f64((uint64_t)(e + 1023) << 52);
  * kernels are latency-bound on these chains), then an exact (or
  * single-rounding, for subnormal results) scale by 2^k. Written without
  * branches: special inputs are resolved by selects at the end. */
+/* e^r for |r| <= ln2/2: the degree-13 Taylor polynomial by Estrin's scheme,
+ * every pair a + b x one fused multiply-add */
+HYG_HD double hyg__exp_poly(double r) {
+  const double r2 = r * r;
+  const double r4 = r2 * r2;
+  const double r8 = r4 * r4;
+  const double q0 = HYG_FMA(1.0, r, 1.0);
+  const double q1 = HYG_FMA(1.6666666666666665741e-01, r, 0.5);                   /* 1/2!, 1/3! */
+  const double q2 = HYG_FMA(8.3333333333333332177e-03, r, 4.1666666666666664354e-02); /* 1/4!, 1/5! */
+  const double q3 = HYG_FMA(1.9841269841269841253e-04, r, 1.3888888888888888889e-03); /* 1/6!, 1/7! */
+  const double q4 = HYG_FMA(2.7557319223985890653e-06, r, 2.4801587301587301566e-05); /* 1/8!, 1/9! */
+  const double q5 = HYG_FMA(2.5052108385441718775e-08, r, 2.7557319223985890653e-07); /* 1/10!, 1/11! */
+  const double q6 = HYG_FMA(1.6059043836821614599e-10, r, 2.0876756987868098979e-09); /* 1/12!, 1/13! */
+  const double s0 = HYG_FMA(q1, r2, q0);
+  const double s1 = HYG_FMA(q3, r2, q2);
+  const double s2 = HYG_FMA(q5, r2, q4);
+  const double u0 = HYG_FMA(s1, r4, s0);
+  const double u1 = HYG_FMA(q6, r4, s2);
+  return HYG_FMA(u1, r8, u0);
+}
 HYG_HD double hyg_exp(double x) {
   const double xc = HYG_FMIN(HYG_FMAX(x, -746.0), 710.0); /* NaN -> -746 (result selected below) */
   const double kd = HYG_FLOOR(xc * HYG_INV_LN2 + 0.5);
   const int k = (int)kd;
-  const double hi = xc - kd * HYG_LN2_HI;
-  const double lo = kd * HYG_LN2_LO;
-  const double r = hi - lo;
-  const double r2 = r * r;
-  const double r4 = r2 * r2;
-  const double r8 = r4 * r4;
-  const double q0 = 1.0 + 1.0 * r;
-  const double q1 = 0.5 + 1.6666666666666665741e-01 * r;                   /* 1/2!, 1/3! */
-  const double q2 = 4.1666666666666664354e-02 + 8.3333333333333332177e-03 * r; /* 1/4!, 1/5! */
-  const double q3 = 1.3888888888888888889e-03 + 1.9841269841269841253e-04 * r; /* 1/6!, 1/7! */
-  const double q4 = 2.4801587301587301566e-05 + 2.7557319223985890653e-06 * r; /* 1/8!, 1/9! */
-  const double q5 = 2.7557319223985890653e-07 + 2.5052108385441718775e-08 * r; /* 1/10!, 1/11! */
-  const double q6 = 2.0876756987868098979e-09 + 1.6059043836821614599e-10 * r; /* 1/12!, 1/13! */
-  const double s0 = q0 + q1 * r2;
-  const double s1 = q2 + q3 * r2;
-  const double s2 = q4 + q5 * r2;
-  const double u0 = s0 + s1 * r4;
-  const double u1 = s2 + q6 * r4;
-  const double p = u0 + u1 * r8;
+  const double hi = xc - kd * HYG_LN2_HI;         /* exact */
+  const double r = HYG_FMA(-kd, HYG_LN2_LO, hi);   /* one rounding */
+  const double p = hyg__exp_poly(r);
   /* k > 1023: (p*2) 2^(k-1); k >= -1021: p 2^k; else (p 2^(k+54)) 2^-54 */
   const int big = k > 1023, sub = k < -1021;
   const int k1 = big ? k - 1 : (sub ? k + 54 : k);
@@ -154,21 +165,21 @@ HYG_HD double hyg_log(double x) {
   const double z4 = z2 * z2;
   const double z8 = z4 * z4;
   /* R/z = sum_{i=0}^{10} a_i z^i, a_i = 2/(2i+3) */
-  const double a01 = 0.66666666666666666667 + 0.40000000000000000000 * z;
-  const double a23 = 0.28571428571428571429 + 0.22222222222222222222 * z;
-  const double a45 = 0.18181818181818181818 + 0.15384615384615384615 * z;
-  const double a67 = 0.13333333333333333333 + 0.11764705882352941176 * z;
-  const double a89 = 0.10526315789473684211 + 0.09523809523809523810 * z;
+  const double a01 = HYG_FMA(0.40000000000000000000, z, 0.66666666666666666667);
+  const double a23 = HYG_FMA(0.22222222222222222222, z, 0.28571428571428571429);
+  const double a45 = HYG_FMA(0.15384615384615384615, z, 0.18181818181818181818);
+  const double a67 = HYG_FMA(0.11764705882352941176, z, 0.13333333333333333333);
+  const double a89 = HYG_FMA(0.09523809523809523810, z, 0.10526315789473684211);
   const double a10 = 0.08695652173913043478;
-  const double b0 = a01 + a23 * z2;
-  const double b1 = a45 + a67 * z2;
-  const double b2 = a89 + a10 * z2;
-  const double c0 = b0 + b1 * z4;
-  const double R = z * (c0 + b2 * z8);
+  const double b0 = HYG_FMA(a23, z2, a01);
+  const double b1 = HYG_FMA(a67, z2, a45);
+  const double b2 = HYG_FMA(a10, z2, a89);
+  const double c0 = HYG_FMA(b1, z4, b0);
+  const double R = z * HYG_FMA(b2, z8, c0);
   const double hfsq = 0.5 * f * f;
-  const double l1p = f - (hfsq - s * (hfsq + R));
+  const double l1p = f - HYG_FMA(-s, hfsq + R, hfsq);
   const double ed = (double)e;
-  double v = ed * HYG_LN2_HI + (ed * HYG_LN2_LO + l1p);
+  double v = HYG_FMA(ed, HYG_LN2_HI, HYG_FMA(ed, HYG_LN2_LO, l1p));
   v = ((b >> 52) == 0x7ff) ? xs : v; /* +inf */
   v = (x == 0.0) ? HYG_NINF : v;
   return (x != x || x < 0.0) ? HYG_NAN : v;
@@ -187,15 +198,15 @@ HYG_HD float hyg_expf(float x) {
    * -104, 89 and the floor of an f32 value are f32 values) */
   const float xc = HYG_FMINF(HYG_FMAXF(x, -104.0f), 89.0f); /* NaN -> -104 */
   const float kf = HYG_FLOORF(xc * 0x1.715476p+0f + 0.5f);
-  const float hi = xc - kf * 0x1.62e4p-1f;
-  const float r = hi - kf * 0x1.7f7d1cp-20f;
+  const float hi = xc - kf * 0x1.62e4p-1f;                  /* exact */
+  const float r = HYG_FMAF(-kf, 0x1.7f7d1cp-20f, hi);       /* one rounding */
   const float r2 = r * r;
   const float r4 = r2 * r2;
   const float q0 = 1.0f + r;
-  const float q1 = 0.5f + 0x1.555556p-3f * r;           /* 1/2!, 1/3! */
-  const float q2 = 0x1.555556p-5f + 0x1.111112p-7f * r; /* 1/4!, 1/5! */
-  const float q3 = 0x1.6c16c2p-10f + 0x1.a01a02p-13f * r; /* 1/6!, 1/7! */
-  const float p = (q0 + q1 * r2) + (q2 + q3 * r2) * r4;
+  const float q1 = HYG_FMAF(0x1.555556p-3f, r, 0.5f);           /* 1/2!, 1/3! */
+  const float q2 = HYG_FMAF(0x1.111112p-7f, r, 0x1.555556p-5f); /* 1/4!, 1/5! */
+  const float q3 = HYG_FMAF(0x1.a01a02p-13f, r, 0x1.6c16c2p-10f); /* 1/6!, 1/7! */
+  const float p = HYG_FMAF(HYG_FMAF(q3, r2, q2), r4, HYG_FMAF(q1, r2, q0));
   const int k = (int)kf;
   const int big = k > 127, sub = k < -126;
   const int k1 = big ? k - 1 : (sub ? k + 64 : k);
@@ -302,24 +313,8 @@ HYG_HD hyg_u128 hyg_exp_fix100(double x) {
   const double kd = HYG_FLOOR(xc * HYG_INV_LN2 + 0.5);
   const int k = (int)kd;
   const double hi = xc - kd * HYG_LN2_HI;
-  const double lo = kd * HYG_LN2_LO;
-  const double r = hi - lo;
-  const double r2 = r * r;
-  const double r4 = r2 * r2;
-  const double r8 = r4 * r4;
-  const double q0 = 1.0 + 1.0 * r;
-  const double q1 = 0.5 + 1.6666666666666665741e-01 * r;
-  const double q2 = 4.1666666666666664354e-02 + 8.3333333333333332177e-03 * r;
-  const double q3 = 1.3888888888888888889e-03 + 1.9841269841269841253e-04 * r;
-  const double q4 = 2.4801587301587301566e-05 + 2.7557319223985890653e-06 * r;
-  const double q5 = 2.7557319223985890653e-07 + 2.5052108385441718775e-08 * r;
-  const double q6 = 2.0876756987868098979e-09 + 1.6059043836821614599e-10 * r;
-  const double s0 = q0 + q1 * r2;
-  const double s1 = q2 + q3 * r2;
-  const double s2 = q4 + q5 * r2;
-  const double u0 = s0 + s1 * r4;
-  const double u1 = s2 + q6 * r4;
-  const double p = u0 + u1 * r8;
+  const double r = HYG_FMA(-kd, HYG_LN2_LO, hi);
+  const double p = hyg__exp_poly(r);
   return hyg_exp_fix100_pk(p, k, x);
 }
 

@@ -3,9 +3,10 @@
 A second, language-independent implementation of the same reference algorithm
 as oracle/tg_oracle.c, used only by tests to cross-check the C oracle bit for
 bit on small chains (T ~ 100, M ~ 10). It re-implements the arithmetic
-contract of include/hyg_arith.h itself (Python floats are IEEE doubles with no
-FMA; numpy float32 scalars give IEEE single ops; Python ints make the exact
-mass sums trivially exact) and reads only the model TABLES from the C side
+contract of include/hyg_arith.h itself (Python floats are IEEE doubles; the
+contract's explicit fused multiply-adds are computed exactly with Python
+integers and rounded once (det_fma / det_fmaf); numpy float32 scalars give IEEE
+single ops; Python ints make the exact mass sums trivially exact) and reads only the model TABLES from the C side
 (constants and hazard), which tests/test_model_tables.py pins against scipy.
 
 Reference (src/two_group/hygeia): filter_and_smoother_algorithm.py:141-288
@@ -41,6 +42,52 @@ def _pow2(e: int) -> float:
     return math.ldexp(1.0, e)
 
 
+def _exact(x: float):
+    """finite double x = m 2^e with integer m"""
+    m, e = math.frexp(x)
+    return int(m * (1 << 53)), e - 53
+
+
+def _exact_sum(a, b, c):
+    """a * b + c exactly, as an integer mantissa and exponent (finite inputs)"""
+    ma, ea = _exact(float(a))
+    mb, eb = _exact(float(b))
+    mc, ec = _exact(float(c))
+    mp, ep = ma * mb, ea + eb
+    e0 = min(ep, ec)
+    return (mp << (ep - e0)) + (mc << (ec - e0)), e0
+
+
+def det_fma(a: float, b: float, c: float) -> float:
+    """IEEE fma (one rounding) of finite doubles: the exact a b + c as a Python
+    integer, rounded once (int -> float conversion is correctly rounded; the
+    exponent scaling is exact for the normal results the contract uses)."""
+    m, e = _exact_sum(a, b, c)
+    if m == 0:
+        return a * b + c
+    return math.ldexp(float(m), e)
+
+
+def det_fmaf(a, b, c) -> np.float32:
+    """IEEE fmaf (one rounding to binary32, ties to even) of float32 values."""
+    m, e = _exact_sum(a, b, c)
+    if m == 0:
+        return np.float32(np.float32(a) * np.float32(b) + np.float32(c))
+    neg = m < 0
+    m = -m if neg else m
+    shift = m.bit_length() - 24
+    if e + shift < -149:  # subnormal result: the lsb is 2^-149
+        shift = -149 - e
+    if shift > 0:
+        q, r = divmod(m, 1 << shift)
+        half = 1 << (shift - 1)
+        if r > half or (r == half and (q & 1)):
+            q += 1
+        m, e = q, e + shift
+    v = np.float32(math.ldexp(float(m), e))  # exact: <= 24 significant bits
+    return -v if neg else v
+
+
 def det_exp(x: float) -> float:
     """hyg_exp: Taylor degree 13 by Estrin's scheme (same operations, same order)."""
     if x != x:
@@ -51,9 +98,8 @@ def det_exp(x: float) -> float:
         return 0.0
     kd = math.floor(x * _INV_LN2 + 0.5)
     k = int(kd)
-    hi = x - kd * _LN2_HI
-    lo = kd * _LN2_LO
-    r = hi - lo
+    hi = x - kd * _LN2_HI  # exact
+    r = det_fma(-kd, _LN2_LO, hi)
     r2 = r * r
     r4 = r2 * r2
     r8 = r4 * r4
@@ -61,13 +107,13 @@ def det_exp(x: float) -> float:
          1.3888888888888888889e-03, 1.9841269841269841253e-04, 2.4801587301587301566e-05,
          2.7557319223985890653e-06, 2.7557319223985890653e-07, 2.5052108385441718775e-08,
          2.0876756987868098979e-09, 1.6059043836821614599e-10]
-    q = [c[2 * i] + c[2 * i + 1] * r for i in range(7)]
-    s0 = q[0] + q[1] * r2
-    s1 = q[2] + q[3] * r2
-    s2 = q[4] + q[5] * r2
-    u0 = s0 + s1 * r4
-    u1 = s2 + q[6] * r4
-    p = u0 + u1 * r8
+    q = [det_fma(c[2 * i + 1], r, c[2 * i]) for i in range(7)]
+    s0 = det_fma(q[1], r2, q[0])
+    s1 = det_fma(q[3], r2, q[2])
+    s2 = det_fma(q[5], r2, q[4])
+    u0 = det_fma(s1, r4, s0)
+    u1 = det_fma(q[6], r4, s2)
+    p = det_fma(u1, r8, u0)
     if k > 1023:
         return (p * 2.0) * _pow2(k - 1)
     if k >= -1021:
@@ -98,21 +144,21 @@ def det_log(x: float) -> float:
     a = [0.66666666666666666667, 0.40000000000000000000, 0.28571428571428571429, 0.22222222222222222222,
          0.18181818181818181818, 0.15384615384615384615, 0.13333333333333333333, 0.11764705882352941176,
          0.10526315789473684211, 0.09523809523809523810]
-    a01 = a[0] + a[1] * z
-    a23 = a[2] + a[3] * z
-    a45 = a[4] + a[5] * z
-    a67 = a[6] + a[7] * z
-    a89 = a[8] + a[9] * z
+    a01 = det_fma(a[1], z, a[0])
+    a23 = det_fma(a[3], z, a[2])
+    a45 = det_fma(a[5], z, a[4])
+    a67 = det_fma(a[7], z, a[6])
+    a89 = det_fma(a[9], z, a[8])
     a10 = 0.08695652173913043478
-    b0 = a01 + a23 * z2
-    b1 = a45 + a67 * z2
-    b2 = a89 + a10 * z2
-    c0 = b0 + b1 * z4
-    R = z * (c0 + b2 * z8)
+    b0 = det_fma(a23, z2, a01)
+    b1 = det_fma(a67, z2, a45)
+    b2 = det_fma(a10, z2, a89)
+    c0 = det_fma(b1, z4, b0)
+    R = z * det_fma(b2, z8, c0)
     hfsq = 0.5 * f * f
-    l1p = f - (hfsq - s * (hfsq + R))
+    l1p = f - det_fma(-s, hfsq + R, hfsq)
     ed = float(e)
-    return ed * _LN2_HI + (ed * _LN2_LO + l1p)
+    return det_fma(ed, _LN2_HI, det_fma(ed, _LN2_LO, l1p))
 
 
 def f32(x) -> np.float32:
@@ -138,14 +184,14 @@ def det_expf(x: np.float32) -> np.float32:
     c = _EXPF_C
     one, half = np.float32(1.0), np.float32(0.5)
     kf = np.float32(math.floor(float(x * c["log2e"] + half)))
-    r = (x - kf * c["hi"]) - kf * c["lo"]
+    r = det_fmaf(-kf, c["lo"], x - kf * c["hi"])
     r2 = r * r
     r4 = r2 * r2
     q0 = one + r
-    q1 = half + c["c3"] * r
-    q2 = c["c4"] + c["c5"] * r
-    q3 = c["c6"] + c["c7"] * r
-    p = (q0 + q1 * r2) + (q2 + q3 * r2) * r4
+    q1 = det_fmaf(c["c3"], r, half)
+    q2 = det_fmaf(c["c5"], r, c["c4"])
+    q3 = det_fmaf(c["c7"], r, c["c6"])
+    p = det_fmaf(det_fmaf(q3, r2, q2), r4, det_fmaf(q1, r2, q0))
     k = int(kf)
     if k > 127:
         return p * np.float32(2.0) * np.float32(2.0 ** (k - 1))
