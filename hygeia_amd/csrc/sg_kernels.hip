@@ -600,151 +600,165 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         const double* wP = w_ + pb * NT;
         if (fin > M) {
           // optimalFiniteState (resample.h:289-409) on the weights sorted
-          // descending. The K loop needs only the sorted values: when w is
-          // non-increasing along the log-weight order, that order carries
-          // them; otherwise (or for the index order the optimal branch
-          // assigns) the exact sort by w, ties by index, is run.
+          // descending, ties by index. The log-weight order already is that
+          // order when every adjacent pair along it has w decreasing, or w
+          // equal and the indices ascending (a total order is checked by its
+          // adjacent pairs); otherwise the exact sort by w runs. Either way
+          // idx is the order the optimal branch assigns: no second sort there.
+          // Ties among zero weights may stand in any order: w = exp(lw - log Z)
+          // is monotone, so they fill the same tail positions in both orders,
+          // and the branch never references a zero-weight entry (K counts
+          // log q > -c only, a systematic draw lands on positive mass only).
           double q = (tid < Np) ? wP[lidx] : 0.0;
-          if (tid < NT) logq[tid] = q;
-          lds_barrier();
-          const bool mono = !block_or<NB>(tid + 1 < Np && logq[tid + 1] > q, red);
-          if (!PE) { SG_PH(13); }
-          int idx = lidx;
-          if (!mono) {
-            uint64_t key = (tid < Np) ? sg_okey(pw) : 0;
-            idx = tid;
-            sg_bitonic<NB>(key, idx, xk, xi);
-            q = (tid < Np) ? sg_okey_value(key) : 0.0;
-          }
-          double lq = HYG_NINF;
-          hyg_u128 mq = hyg_u128_zero();
-          if (tid < Np) {
-            lq = hyg_log(q);
-            mq = hyg_fix100(q);
-          }
           if (tid < NT) {
-            logq[tid] = lq;
-            sidx[tid] = idx;
-          }
-          // reverse cumulative sums Q(k) = total - exclusive prefix (exact)
-          block_scan128<NB>(mq, cum, red);
-          if (!PE) { SG_PH(14); }
-          lds_barrier();
-          {
-            const hyg_u128 tot = cum[NB], ex = cum[tid];
-            hyg_u128 suf;
-            suf.lo = tot.lo - ex.lo;
-            suf.hi = tot.hi - ex.hi - (tot.lo < ex.lo ? 1u : 0u);
-            lds_barrier();
-            cum[tid] = suf;
-            if (tid <= NT) logQ[tid] = hyg_log(hyg_u128_to_f64(suf, 100));
-            if (NB == NT && tid == 0) logQ[NT] = HYG_NINF;
+            logq[tid] = q;
+            sidx[tid] = lidx;
           }
           lds_barrier();
-          SG_PH(1);
-          // the K / log c fixed point (:333-342). When log q is non-increasing
-          // along the sorted order (checked; log is only nearly monotone), the
-          // count #{p >= a : log q_p > -c(a)} is a prefix length: every a in
-          // [0, Np] gets c(a) and its successor next(a) by a binary search at
-          // once, then one lane follows a -> next(a) from 0 to the fixed point
-          // (the loop's iterates, so K and log c are the loop's). Otherwise the
-          // loop runs in wave 0 with counts by ballot.
-          const bool lqmono = !block_or<NB>(tid + 1 < Np && logq[tid + 1] > logq[tid], red);
-          if (lqmono) {
-            double* cval = (double*)cum;           // [NT + 1] c(a)
-            int* nxt = (int*)(cval + NT + 1);      // [NT + 1] next(a)
-            for (int a = tid; a <= Np; a += NB) {
-              const int mk = M - a;
-              const double cA = (mk >= 0 ? logm[mk] : HYG_NAN) - logQ[a];
-              const double thr = -cA;
-              int lo = 0, hi = Np;  // first p with !(log q_p > thr)
-              while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (logq[mid] > thr) lo = mid + 1; else hi = mid;
-              }
-              nxt[a] = a + (lo > a ? lo - a : 0);
-              cval[a] = cA;
-            }
-            lds_barrier();
-            if (tid == 0) {
-              int kOld = 1, kNew = 0, iters = 0;
-              while (kNew != kOld) {
-                kOld = kNew;
-                kNew = nxt[kOld];
-                ++iters;
-              }
-              sh.Kk = kNew;
-              sh.logC = cval[kOld];
-              SG_CNT(10, iters);
-            }
-          } else if (wv == 0) {
-            double lq4[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) lq4[i] = logq[lane + 64 * i];
-            int kOld = 1, kNew = 0, iters = 0;
-            double logC = 0.0;
-            while (kNew != kOld) {
-              kOld = kNew;
-              // hyg_log(M - kOld) - hyg_log(Q(kOld)) from the tables (log of a negative count is NaN)
-              const int mk = M - kOld;
-              logC = (mk >= 0 ? logm[mk] : HYG_NAN) - logQ[kOld];
-              const double thr = -logC;
-              int cnt = 0;
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int p = lane + 64 * i;
-                cnt += __builtin_popcountll(__ballot(p >= kOld && p < Np && lq4[i] > thr));
-              }
-              kNew = kOld + cnt;
-              ++iters;
-            }
-            if (lane == 0) {
-              sh.Kk = kNew;
-              sh.logC = logC;
-            }
-            SG_CNT(10, iters);
-          }
-          lds_barrier();
-          SG_PH(2);
-          const double logC = sh.logC;
-          if (hyg_isfinite(logC)) {
-            keep_top = false;
-            if (mono) {  // the exact index order among equal weights
+          bool disorder;
+          int nz;  // weights with a nonzero F = 100 image
+          block_or_count<NB>(
+              tid + 1 < Np && !(q > logq[tid + 1] || (q == logq[tid + 1] && (lidx < sidx[tid + 1] || q == 0.0))),
+              tid < Np && q >= 0x1p-100, red, &disorder, &nz);
+          if (!PE) { SG_PH(13); }
+          // Fewer than M weights with a nonzero image: the K loop provably ends
+          // in the keep-top fallback, so it is not run. At an iterate k < nz,
+          // the exact suffix Q(k) <= (nz - k) q_k <= (M - 1 - k) q_k, so
+          // log q_k - (log Q(k) - log(M - k)) >= log((M - k) / (M - 1 - k)) >=
+          // 1/256, far above the rounding of the logs: q_k is counted and k
+          // grows. Once k >= nz, Q(k) = 0 and log c is +inf or NaN, never finite.
+          if (nz >= M) {
+            int idx = lidx;
+            if (disorder) {
               uint64_t key = (tid < Np) ? sg_okey(pw) : 0;
               idx = tid;
               sg_bitonic<NB>(key, idx, xk, xi);
-              if (tid < NT) sidx[tid] = idx;
+              q = (tid < Np) ? sg_okey_value(key) : 0.0;
             }
-            const int Kk = sh.Kk, L = M - Kk;
-            if (tid < Kk) {
-              anc[tid] = idx;
-              lwres[tid] = lwP[idx];
+            double lq = HYG_NINF;
+            hyg_u128 mq = hyg_u128_zero();
+            if (tid < Np) {
+              lq = hyg_log(q);
+              mq = hyg_fix100(q);
             }
-            if (L > 0) {
-              // residual systematic draw (:372-377, systematicBase :85-117):
-              // T_j = (j + u) / L <= Q_i as exact C_i >= ceil(T_j R)
-              const bool inres = tid >= Kk && tid < Np;
-              const double rmax = block_max<NB>(inres ? lq : HYG_NINF, red);
-              const hyg_u128 m2 = inres ? hyg_exp_fix100(lq - rmax) : hyg_u128_zero();
-              block_scan128<NB>(m2, cum, red);
-              const hyg_u128 incl = hyg_u128_add(cum[tid], m2);
+            if (tid < NT) {
+              logq[tid] = lq;
+              sidx[tid] = idx;
+            }
+            // reverse cumulative sums Q(k) = total - exclusive prefix (exact)
+            block_scan128<NB>(mq, cum, red);
+            if (!PE) { SG_PH(14); }
+            lds_barrier();
+            {
+              const hyg_u128 tot = cum[NB], ex = cum[tid];
+              hyg_u128 suf;
+              suf.lo = tot.lo - ex.lo;
+              suf.hi = tot.hi - ex.hi - (tot.lo < ex.lo ? 1u : 0u);
               lds_barrier();
-              cum[tid] = incl;
-              lds_barrier();
-              const hyg_u128 R = cum[Np - 1];
-              if (tid < L) {
-                const double uu =
-                    (double)(hyg_rand64(ch.seed, ch.chain_id, kSgRngSystematic, (uint64_t)t, 0) >> 11) *
-                    1.1102230246251565404e-16;
-                const double Tj = ((double)tid + uu) / (double)L;
-                const hyg_u128 thr = sg_ceil_mul_f64(Tj, R);
-                int lo = Kk, hi = Np - 1;
+              cum[tid] = suf;
+              if (tid <= NT) logQ[tid] = hyg_log(hyg_u128_to_f64(suf, 100));
+              if (NB == NT && tid == 0) logQ[NT] = HYG_NINF;
+            }
+            lds_barrier();
+            SG_PH(1);
+            // the K / log c fixed point (:333-342). When log q is non-increasing
+            // along the sorted order (checked; log is only nearly monotone), the
+            // count #{p >= a : log q_p > -c(a)} is a prefix length: every a in
+            // [0, Np] gets c(a) and its successor next(a) by a binary search at
+            // once, then one lane follows a -> next(a) from 0 to the fixed point
+            // (the loop's iterates, so K and log c are the loop's). Otherwise the
+            // loop runs in wave 0 with counts by ballot.
+            const bool lqmono = !block_or<NB>(tid + 1 < Np && logq[tid + 1] > logq[tid], red);
+            if (lqmono) {
+              double* cval = (double*)cum;           // [NT + 1] c(a)
+              int* nxt = (int*)(cval + NT + 1);      // [NT + 1] next(a)
+              for (int a = tid; a <= Np; a += NB) {
+                const int mk = M - a;
+                const double cA = (mk >= 0 ? logm[mk] : HYG_NAN) - logQ[a];
+                const double thr = -cA;
+                int lo = 0, hi = Np;  // first p with !(log q_p > thr)
                 while (lo < hi) {
                   const int mid = (lo + hi) >> 1;
-                  if (hyg_u128_lt(cum[mid], thr)) lo = mid + 1; else hi = mid;
+                  if (logq[mid] > thr) lo = mid + 1; else hi = mid;
                 }
-                anc[Kk + tid] = sidx[lo];
-                lwres[Kk + tid] = logZp - logC;
+                nxt[a] = a + (lo > a ? lo - a : 0);
+                cval[a] = cA;
+              }
+              lds_barrier();
+              if (tid == 0) {
+                int kOld = 1, kNew = 0, iters = 0;
+                while (kNew != kOld) {
+                  kOld = kNew;
+                  kNew = nxt[kOld];
+                  ++iters;
+                }
+                sh.Kk = kNew;
+                sh.logC = cval[kOld];
+                SG_CNT(10, iters);
+              }
+            } else if (wv == 0) {
+              double lq4[4];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) lq4[i] = logq[lane + 64 * i];
+              int kOld = 1, kNew = 0, iters = 0;
+              double logC = 0.0;
+              while (kNew != kOld) {
+                kOld = kNew;
+                // hyg_log(M - kOld) - hyg_log(Q(kOld)) from the tables (log of a negative count is NaN)
+                const int mk = M - kOld;
+                logC = (mk >= 0 ? logm[mk] : HYG_NAN) - logQ[kOld];
+                const double thr = -logC;
+                int cnt = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const int p = lane + 64 * i;
+                  cnt += __builtin_popcountll(__ballot(p >= kOld && p < Np && lq4[i] > thr));
+                }
+                kNew = kOld + cnt;
+                ++iters;
+              }
+              if (lane == 0) {
+                sh.Kk = kNew;
+                sh.logC = logC;
+              }
+              SG_CNT(10, iters);
+            }
+            lds_barrier();
+            SG_PH(2);
+            const double logC = sh.logC;
+            if (hyg_isfinite(logC)) {
+              keep_top = false;
+              const int Kk = sh.Kk, L = M - Kk;
+              if (tid < Kk) {
+                anc[tid] = idx;
+                lwres[tid] = lwP[idx];
+              }
+              if (L > 0) {
+                // residual systematic draw (:372-377, systematicBase :85-117):
+                // T_j = (j + u) / L <= Q_i as exact C_i >= ceil(T_j R)
+                const bool inres = tid >= Kk && tid < Np;
+                const double rmax = block_max<NB>(inres ? lq : HYG_NINF, red);
+                const hyg_u128 m2 = inres ? hyg_exp_fix100(lq - rmax) : hyg_u128_zero();
+                block_scan128<NB>(m2, cum, red);
+                const hyg_u128 incl = hyg_u128_add(cum[tid], m2);
+                lds_barrier();
+                cum[tid] = incl;
+                lds_barrier();
+                const hyg_u128 R = cum[Np - 1];
+                if (tid < L) {
+                  const double uu =
+                      (double)(hyg_rand64(ch.seed, ch.chain_id, kSgRngSystematic, (uint64_t)t, 0) >> 11) *
+                      1.1102230246251565404e-16;
+                  const double Tj = ((double)tid + uu) / (double)L;
+                  const hyg_u128 thr = sg_ceil_mul_f64(Tj, R);
+                  int lo = Kk, hi = Np - 1;
+                  while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (hyg_u128_lt(cum[mid], thr)) lo = mid + 1; else hi = mid;
+                  }
+                  anc[Kk + tid] = sidx[lo];
+                  lwres[Kk + tid] = logZp - logC;
+                }
               }
             }
           }
@@ -805,9 +819,22 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       }
       double* redd = (double*)red;
       hyg_u128* redu = (hyg_u128*)(red + 8 * NW * K);
+      // the continuing particles' part of the block max and finite count of
+      // the new log-weights rides on this reduction's barrier; the fresh
+      // particles' part is added from lsev below (no reduction of its own)
+      double* redc = (double*)(red + 24 * NW * K);
+      int* redn = (int*)(redc + NW);
       double mq[KH];
 #pragma unroll
       for (int j = 0; j < KH; ++j) mq[j] = wave_max(vb[j]);
+      {
+        const double cm = wave_max(nlw);  // -inf beyond the continuing particles
+        const int cn = __builtin_popcountll(wave_ballot(tid < M && hyg_isfinite(nlw)));
+        if (lane == 0) {
+          redc[wv] = cm;
+          redn[wv] = cn;
+        }
+      }
       if (lane == 0) {  // rows this wave does not take: neutral partials (-inf maxima, zero sums)
 #pragma unroll
         for (int q = 0; q < K; ++q) {
@@ -880,8 +907,23 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       // record t-1 (stored at the end of step t-1) is drained by every wave
       // here, before the barriers of the reductions; published after them
       sg_drain_stores();
-      double mx;
-      block_max_cnt<NB>(nlw, (tid < N && hyg_isfinite(nlw)) ? 1 : 0, red, &mx, &fin);
+      // block max and finite count of the N new log-weights: the continuing
+      // particles' wave partials and the K fresh ones (lsev[q] + log g_t(q), as
+      // formed above), the same values as one block reduction (a max is exact)
+      double mx = redc[0];
+      fin = redn[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        mx = dmax(mx, redc[w]);
+        fin += redn[w];
+      }
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        const double lb = lsev[q];
+        const double f = (lb > HYG_NINF) ? lb + et[q] : HYG_NINF;
+        mx = dmax(mx, f);
+        fin += hyg_isfinite(f) ? 1 : 0;
+      }
       if (!(mx > HYG_NINF)) {
         status = HYG_ENUMERIC;
         break;
