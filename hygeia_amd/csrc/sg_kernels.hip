@@ -103,6 +103,16 @@ struct SgLay {
 
 __host__ __device__ inline size_t sg_align(size_t x) { return (x + 15) / 16 * 16; }
 
+// The SMC workgroup's reduction area: block reductions use its first 32 B per
+// wave; the weights' arrays (continuing-particle partials, A_r, E_r limbs,
+// G[r][q], m_q) live behind them (sg_chain_kernel)
+__host__ __device__ inline size_t sg_red_w(int NW) { return 32 * (size_t)NW; }
+__host__ __device__ inline size_t sg_red_bytes(int K, int NW) {
+  const size_t a = 24 * (size_t)NW * K + 16 * NW + 64;
+  const size_t b = sg_red_w(NW) + 12 * (size_t)NW + 8 + 8 * (size_t)K + 24 * (size_t)K + 8 * (size_t)K * K + 8 * K;
+  return a > b ? a : b;
+}
+
 // NB = threads of the workgroup (particles live on threads < 256, the other
 // waves join the block reductions, sorts (on dummy keys) and the smoothing tasks)
 __host__ __device__ inline int sg_block_threads(int K) { return K <= 8 ? 512 : 256; }
@@ -125,7 +135,7 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap, bool pe) {
   l.xi = o; o = sg_align(o + 4 * 2 * NB);
   l.BK = o; o = sg_align(o + 8 * (size_t)K * NT);
   l.logP = o; o = sg_align(o + 8 * (size_t)K * K);
-  l.red = o; o = sg_align(o + 24 * (size_t)NW * K + 16 * NW + 64);
+  l.red = o; o = sg_align(o + sg_red_bytes(K, NW));
   l.lsev = o; o = sg_align(o + 8 * 2 * (size_t)K);
   l.scr = o; o = sg_align(o + 8 * (size_t)NW * NT);
   l.meanb = o; o = sg_align(o + 8 * (size_t)kSgChunk * K);
@@ -480,6 +490,12 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
   hyg_sgpe_model* pm = PE ? (hyg_sgpe_model*)(smem + lay.pm) : nullptr;
   double* logP = PE ? pm->logP : (double*)(smem + lay.logP);
   unsigned char* red = smem + lay.red;
+  double* redc = (double*)(red + sg_red_w(NW));   // continuing particles: block max partials
+  int* redn = (int*)(redc + NW);                  //   and finite counts (see the normalisation)
+  double* Amax = (double*)(redn + NW + (NW & 1)); // [K] A_r (backward kernels)
+  unsigned long long* Elimb = (unsigned long long*)(Amax + K);  // [K][3] 34-bit limbs of E_r
+  double* Gq = (double*)(Elimb + 3 * K);          // [K][K] G[r][q]
+  double* mqv = Gq + K * K;                       // [K] m_q
   double* lsev = (double*)(smem + lay.lsev);
   double* logm = (double*)(smem + lay.logm);
   double* logQ = (double*)(smem + lay.logQ);
@@ -774,6 +790,11 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         anc[tid] = tid;
         lwres[tid] = plw;
       }
+      // the weights' LDS accumulators, behind this barrier (their last readers
+      // were behind the previous step's last barrier; block reductions do not
+      // touch them)
+      if (tid < K) Amax[tid] = HYG_NINF;
+      if (tid < 3 * K) Elimb[tid] = 0ull;
       lds_barrier();
       SG_PH(3);
       // ---- sampleParticlesCp (:504-522) + computeWeightsCp (:536-574)
@@ -789,18 +810,23 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         nst = sg_pack(sg_d(sa) + 1, r);
         nlw = lwres[tid] + (contP[a] + e);
       }
-      // backward kernels (:288-326) K_q(n) = exp(x_qn - max_q) / S_q with
-      // x_qn = W_prev[n] + log f((1,q) | n), and the fresh particles (1, q) with
-      // log weight max_q + log S_q + log g_t(q): thread n = previous particle n,
-      // the K row reductions batched (oracle/sg_oracle.c)
+      // backward kernels (:288-326), factorised over the regimes as in
+      // oracle/sg_oracle.c: a_n = W_prev[n] + b_n (b_n + log P[r_n][q] = log
+      // f((1,q) | n)), A_r = max of a_n over regime r, m_q = max_r (A_r + log
+      // P[r][q]), K_q(n) = (e_n G[r_n][q]) / S_q with e_n = exp(a_n - A_{r_n}),
+      // G[r][q] = exp((A_r + log P[r][q]) - m_q), S_q = sum_r G[r][q] E_r (E_r:
+      // the exact image sum of e_n over regime r); the fresh particle (1, q)
+      // has log weight m_q + log S_q + log g_t(q). Per particle one exp, an
+      // LDS max and three limb adds (exact, order-free), K^2 exps per step.
       // With 512 threads (K <= 8) thread n < 256 takes rows [0, KH) of previous
-      // particle n and thread 256 + n rows [KH, K) (its particle read from LDS):
-      // half of the rows per thread, same values, exact sums.
+      // particle n and thread 256 + n rows [KH, K) (it recomputes e_n); threads
+      // 256 .. 256 + K^2 form G.
       constexpr bool SPLIT = (NB == 2 * NT);
       constexpr int KH = SPLIT ? (K + 1) / 2 : K;
       const int pn = SPLIT ? (tid & (NT - 1)) : tid;  // the previous particle of this thread
       const int q0 = (SPLIT && tid >= NT) ? KH : 0;   // wave-uniform
-      double vb[KH];
+      double va;
+      int vr;
       {
         double vlw = plw, vbase = pbase;
         uint32_t vst = pst;
@@ -809,25 +835,15 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
           vbase = base_[pb * NT + pn];
           vst = stP[pn];
         }
-        const bool live = pn < Np;
-        const int rp = sg_r(vst);
-#pragma unroll
-        for (int j = 0; j < KH; ++j) {
-          const int q = q0 + j;
-          vb[j] = (live && q < K) ? vlw + (vbase + logP[rp * K + q]) : HYG_NINF;
-        }
+        va = (pn < Np) ? vlw + vbase : HYG_NINF;
+        vr = (va > HYG_NINF) ? sg_r(vst) : 0;  // (no weight: any valid row of G, times e_n = 0)
       }
-      double* redd = (double*)red;
-      hyg_u128* redu = (hyg_u128*)(red + 8 * NW * K);
-      // the continuing particles' part of the block max and finite count of
-      // the new log-weights rides on this reduction's barrier; the fresh
-      // particles' part is added from lsev below (no reduction of its own)
-      double* redc = (double*)(red + 24 * NW * K);
-      int* redn = (int*)(redc + NW);
-      double mq[KH];
-#pragma unroll
-      for (int j = 0; j < KH; ++j) mq[j] = wave_max(vb[j]);
+      if (tid < NT && va > HYG_NINF)
+        __hip_atomic_fetch_max(Amax + vr, va, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       {
+        // the continuing particles' part of the block max and finite count of
+        // the new log-weights rides on this barrier; the fresh particles' part
+        // is added from lsev below (no reduction of its own)
         const double cm = wave_max(nlw);  // -inf beyond the continuing particles
         const int cn = __builtin_popcountll(wave_ballot(tid < M && hyg_isfinite(nlw)));
         if (lane == 0) {
@@ -835,54 +851,44 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
           redn[wv] = cn;
         }
       }
-      if (lane == 0) {  // rows this wave does not take: neutral partials (-inf maxima, zero sums)
-#pragma unroll
-        for (int q = 0; q < K; ++q) {
-          double v = HYG_NINF;
-#pragma unroll
-          for (int j = 0; j < KH; ++j) v = (q0 + j == q) ? mq[j] : v;
-          redd[wv * K + q] = v;
-        }
-      }
       lds_barrier();
-#pragma unroll
-      for (int j = 0; j < KH; ++j) {
-        const int q = q0 + j < K ? q0 + j : K - 1;
-        double m = redd[q];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) m = dmax(m, redd[w * K + q]);
-        mq[j] = (q0 + j < K) ? m : HYG_NINF;
+      const double ea = (va > HYG_NINF) ? hyg_exp(va - Amax[vr]) : 0.0;
+      if (tid < NT && va > HYG_NINF) {
+        const hyg_u128 im = hyg_fix100(ea);  // < 2^101: limbs of 34, 34 and 33 bits
+        unsigned long long* el = Elimb + 3 * vr;
+        constexpr unsigned long long kL = (1ull << 34) - 1;
+        __hip_atomic_fetch_add(el + 0, im.lo & kL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(el + 1, ((im.lo >> 34) | (im.hi << 30)) & kL, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(el + 2, im.hi >> 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      double ev[KH];
       {
-        hyg_u128 s2[KH];
+        const int gi = SPLIT ? tid - NT : tid;  // (r, q) = (gi / K, gi % K)
+        if (gi >= 0 && gi < K * K) {
+          const int r = gi / K, q = gi - (gi / K) * K;
+          double m = HYG_NINF;
 #pragma unroll
-        for (int j = 0; j < KH; ++j) {
-          ev[j] = hyg_exp(vb[j] - mq[j]);
-          s2[j] = hyg_fix100(ev[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < KH; ++j) s2[j] = wave_sum128(s2[j]);
-        if (lane == 0) {
-#pragma unroll
-          for (int q = 0; q < K; ++q) {
-            hyg_u128 v = hyg_u128_zero();
-#pragma unroll
-            for (int j = 0; j < KH; ++j) {
-              v.lo = (q0 + j == q) ? s2[j].lo : v.lo;
-              v.hi = (q0 + j == q) ? s2[j].hi : v.hi;
-            }
-            redu[wv * K + q] = v;
-          }
+          for (int rr = 0; rr < K; ++rr) m = dmax(m, Amax[rr] + logP[rr * K + q]);
+          Gq[gi] = (m > HYG_NINF) ? hyg_exp((Amax[r] + logP[r * K + q]) - m) : 0.0;
+          if (r == 0) mqv[q] = m;
         }
       }
       lds_barrier();
       if (tid < K) {
-        double m = redd[tid];
-        for (int w = 1; w < NW; ++w) m = dmax(m, redd[w * K + tid]);
-        hyg_u128 s = hyg_u128_zero();
-        for (int w = 0; w < NW; ++w) s = hyg_u128_add(s, redu[w * K + tid]);
-        const double S = hyg_u128_to_f64(s, 100);
+        const double m = mqv[tid];
+        double S = 0.0;
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+          const unsigned long long* el = Elimb + 3 * r;
+          // E_r = l0 + l1 2^34 + l2 2^68 (each limb a sum of <= 256 values below 2^34)
+          hyg_u128 e, x;
+          e.lo = el[0]; e.hi = 0;
+          x.lo = el[1] << 34; x.hi = el[1] >> 30;
+          e = hyg_u128_add(e, x);
+          x.lo = 0; x.hi = el[2] << 4;
+          e = hyg_u128_add(e, x);
+          S = HYG_FMA(Gq[r * K + tid], hyg_u128_to_f64(e, 100), S);
+        }
         lsev[tid] = (m > HYG_NINF) ? m + hyg_log(S) : HYG_NINF;  // log-normaliser of row q
         lsev[K + tid] = (m > HYG_NINF) ? 1.0 / S : 0.0;
       }
@@ -890,7 +896,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
 #pragma unroll
       for (int j = 0; j < KH; ++j) {  // this thread's entries of the backward kernels (record of step t)
         const int q = q0 + j < K ? q0 + j : K - 1;
-        BKr[j] = (q0 + j < K && lsev[q] > HYG_NINF) ? ev[j] * lsev[K + q] : 0.0;
+        BKr[j] = (q0 + j < K && lsev[q] > HYG_NINF) ? (ea * Gq[vr * K + q]) * lsev[K + q] : 0.0;
         if (PE && pn < Np && q0 + j < K) BK[q * NT + pn] = BKr[j];
       }
       if (tid >= M && tid < N) {

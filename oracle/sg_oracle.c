@@ -119,6 +119,17 @@ static double sg_trans(sg_model* m, int dc, int rc, int dp, int rp) {
   return -INFINITY;
 }
 
+/* The particle-dependent part b of log f((1, r') | (d, r)) = b + log P[r][r']
+ * (singleGroup.h:569-608): log rho_r(d), 0 once the hazard has exited, -inf
+ * below the minimum sojourn u; as sg_trans forms it (b + log P). */
+static double sg_bpart(sg_model* m, int dp, int rp) {
+  if (dp < m->c.u) return -INFINITY;
+  if (m->pe) return sgm_pe_row(m, dp, rp)->base;
+  int d = dp - 1;
+  if (d >= m->dcap) d = m->dcap - 1;
+  return m->ex[(size_t)rp * m->dcap + d] ? 0.0 : m->hz[((size_t)rp * m->dcap + d) * 2];
+}
+
 /* exact log-sum-exp: max + log(sum fix100(exp(x - max))) */
 static double lse(const double* x, int n) {
   double mx = -INFINITY;
@@ -376,32 +387,56 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
         rC[n] = rP[anc[n]];
         lwC[n] = lwres[n] + (sg_trans(&mo, dC[n], rC[n], dP[anc[n]], rP[anc[n]]) + Et[rC[n]]);
       }
-      /* evaluateBackwardKernels (:288-326): K_q(n) = normalise(W_prev[n] + log f((1,q) | n)),
-       * normalised as exp(x - max) / sum exp(x - max) (one reciprocal per row).
-       * The fresh particle (1, q) has log weight logsumexp_n(W_prev[n] + log f((1,q) | n))
-       * + log g_t(q): the reference's logsumexp_n(log f + log g + W_prev[n])
-       * (computeWeightsCp :563-573) with the n-independent log g taken out. */
-      for (int q = 0; q < K; ++q) {
-        dC[M + q] = 1;
-        rC[M + q] = q;
-        double mx = -INFINITY;
-        for (int n = 0; n < Np; ++n) {
-          tmp[n] = lwP[n] + sg_trans(&mo, 1, q, dP[n], rP[n]);
-          if (tmp[n] > mx) mx = tmp[n];
+      /* evaluateBackwardKernels (:288-326): K_q(n) = normalise_n(W_prev[n] + log f((1,q) | n)).
+       * log f((1,q) | (d_n, r_n)) = b_n + log P[r_n][q] (b_n: the hazard part, sg_bpart;
+       * log P[r][r] = -inf), so with a_n = W_prev[n] + b_n the rows factorise over the
+       * regimes: A_r = max of a_n over the particles of regime r, m_q = max_r (A_r +
+       * log P[r][q]) (= max_n (a_n + log P[r_n][q]): rounding is monotone),
+       *   K_q(n) = (e_n G[r_n][q]) / S_q,  e_n = exp(a_n - A_{r_n}),
+       *   G[r][q] = exp((A_r + log P[r][q]) - m_q),  S_q = sum_r G[r][q] E_r (FMA, r order),
+       * E_r the exact sum of the F = 100 images of e_n over regime r: one exp per
+       * particle and K^2 per step instead of one per (particle, row).
+       * The fresh particle (1, q) has log weight m_q + log S_q + log g_t(q): the
+       * reference's logsumexp_n(log f + log g + W_prev[n]) (computeWeightsCp :563-573)
+       * with the n-independent log g taken out. */
+      {
+        double A[HYG_KMAX], Ef[HYG_KMAX];
+        hyg_u128 Er[HYG_KMAX];
+        for (int r = 0; r < K; ++r) {
+          A[r] = -INFINITY;
+          Er[r] = hyg_u128_zero();
         }
-        if (mx > -INFINITY) {
-          hyg_u128 sacc = hyg_u128_zero();
-          for (int n = 0; n < Np; ++n) {
-            tmp2[n] = hyg_exp(tmp[n] - mx);
-            sacc = hyg_u128_add(sacc, hyg_fix100(tmp2[n]));
+        for (int n = 0; n < Np; ++n) {
+          tmp[n] = lwP[n] + sg_bpart(&mo, dP[n], rP[n]);
+          if (tmp[n] > A[rP[n]]) A[rP[n]] = tmp[n];
+        }
+        for (int n = 0; n < Np; ++n) {
+          tmp2[n] = (tmp[n] > -INFINITY) ? hyg_exp(tmp[n] - A[rP[n]]) : 0.0;
+          Er[rP[n]] = hyg_u128_add(Er[rP[n]], hyg_fix100(tmp2[n]));
+        }
+        for (int r = 0; r < K; ++r) Ef[r] = hyg_u128_to_f64(Er[r], 100);
+        const double* lP = mo.pe ? mo.pm.logP : c->logP;
+        for (int q = 0; q < K; ++q) {
+          dC[M + q] = 1;
+          rC[M + q] = q;
+          double mq = -INFINITY;
+          for (int r = 0; r < K; ++r) {
+            const double v = A[r] + lP[r * K + q];
+            if (v > mq) mq = v;
           }
-          const double S = hyg_u128_to_f64(sacc, 100);
-          const double inv = 1.0 / S;
-          for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = tmp2[n] * inv;
-          lwC[M + q] = (mx + hyg_log(S)) + Et[q];
-        } else {
-          for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = 0.0;
-          lwC[M + q] = -INFINITY;
+          if (mq > -INFINITY) {
+            double G[HYG_KMAX], S = 0.0;
+            for (int r = 0; r < K; ++r) {
+              G[r] = hyg_exp((A[r] + lP[r * K + q]) - mq);
+              S = HYG_FMA(G[r], Ef[r], S);
+            }
+            const double inv = 1.0 / S;
+            for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = (tmp2[n] * G[rP[n]]) * inv;
+            lwC[M + q] = (mq + hyg_log(S)) + Et[q];
+          } else {
+            for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = 0.0;
+            lwC[M + q] = -INFINITY;
+          }
         }
       }
       logZ = lse(lwC, N); /* selfNormaliseWeights (:576-579) */
