@@ -379,28 +379,6 @@ __device__ __forceinline__ bool block_or(bool p, unsigned char* red) {
   return any != 0;
 }
 
-// Block-wide OR of one predicate and count of another, one exchange.
-template <int NT>
-__device__ __forceinline__ void block_or_count(bool p, bool c, unsigned char* red, bool* any_out, int* cnt_out) {
-  const int w = wave_ballot(p) != 0 ? 1 : 0;
-  const int n = __builtin_popcountll(wave_ballot(c));
-  if (NT == 64) { *any_out = w != 0; *cnt_out = n; return; }
-  lds_barrier();
-  if (lane_id() == 0) {
-    ((int*)red)[2 * wave_id()] = w;
-    ((int*)red)[2 * wave_id() + 1] = n;
-  }
-  lds_barrier();
-  int any = 0, cnt = 0;
-#pragma unroll
-  for (int i = 0; i < NT / 64; ++i) {
-    any |= ((int*)red)[2 * i];
-    cnt += ((int*)red)[2 * i + 1];
-  }
-  *any_out = any != 0;
-  *cnt_out = cnt;
-}
-
 // Exclusive block scans. The register forms return this thread's exclusive
 // prefix and the block total; the array form writes out[tid] (exclusive) and
 // out[NT] (total) for searches.

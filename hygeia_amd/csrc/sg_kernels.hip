@@ -630,12 +630,36 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
             logq[tid] = q;
             sidx[tid] = lidx;
           }
+          // adjacent pairs inside a wave after a wave-level hand-off; the pairs
+          // across waves from LDS behind the one barrier of the exchange (the
+          // previous users of red are behind the previous step's last barrier)
+          auto out_of_order = [](double q1, int i1, double q2, int i2) {
+            return !(q1 > q2 || (q1 == q2 && (i1 < i2 || q1 == 0.0)));
+          };
+          wave_lds_sync();
+          bool bad = false;
+          if (tid < NT && lane < 63 && tid + 1 < Np) bad = out_of_order(q, lidx, logq[tid + 1], sidx[tid + 1]);
+          {
+            const int wbad = wave_ballot(bad) != 0 ? 1 : 0;
+            const int wnz = __builtin_popcountll(wave_ballot(tid < Np && q >= 0x1p-100));
+            if (lane == 0) {
+              ((int*)red)[2 * wv] = wbad;
+              ((int*)red)[2 * wv + 1] = wnz;
+            }
+          }
           lds_barrier();
-          bool disorder;
-          int nz;  // weights with a nonzero F = 100 image
-          block_or_count<NB>(
-              tid + 1 < Np && !(q > logq[tid + 1] || (q == logq[tid + 1] && (lidx < sidx[tid + 1] || q == 0.0))),
-              tid < Np && q >= 0x1p-100, red, &disorder, &nz);
+          bool disorder = false;
+          int nz = 0;  // weights with a nonzero F = 100 image
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            disorder = disorder || ((int*)red)[2 * w] != 0;
+            nz += ((int*)red)[2 * w + 1];
+          }
+#pragma unroll
+          for (int w = 0; w + 1 < NT / 64; ++w) {
+            const int p0 = 64 * w + 63;
+            if (p0 + 1 < Np) disorder = disorder || out_of_order(logq[p0], sidx[p0], logq[p0 + 1], sidx[p0 + 1]);
+          }
           if (!PE) { SG_PH(13); }
           // Fewer than M weights with a nonzero image: the K loop provably ends
           // in the keep-top fallback, so it is not run. At an iterate k < nz,
@@ -937,7 +961,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       {
         hyg_u128 fx = hyg_u128_zero();
         if ((NB == NT) || wv < NT / 64) fx = hyg_exp_fix100(nlw - mx);  // waves >= 4 hold no particle
-        logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NB>(fx, red), 100));
+        // (no leading barrier: red's last readers, the weights' partials, are
+        // behind the weights' last barrier)
+        logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NB, false>(fx, red), 100));
       }
       if (tid == 0) sg_st4(ctl, (unsigned)t);  // records 0 .. t-1 are published
       my_lw = nlw;
