@@ -309,13 +309,21 @@ constexpr int kBuckets = 512;  // counting-sort buckets of the resampling sort (
 constexpr int kNCut = 8;       // log-weight cutoffs of the top-set resampling path
 // candidate-list entries per lane per chunk (lse / top-set gather): ~900 list
 // entries at C3 are ~3.5 per lane at 256 threads, under one at 1024
+#ifndef HYG_LR256
+#define HYG_LR256 4
+#endif
 template <int NT>
-constexpr int kLRof = NT >= 512 ? 2 : 4;
+constexpr int kLRof = NT >= 512 ? 2 : HYG_LR256;
 // waves that sort the top set A: at most 256 keys (one per lane of 4 waves)
 // whatever the workgroup size, so a 512- or 1024-thread chain sorts no more
 // keys than a 256-thread one (HYG_SORT_WAVES overrides, for tuning builds)
 #ifndef HYG_SORT_WAVES
 #define HYG_SORT_WAVES 4
+#endif
+// top_set_finish1 (the latency-shaped finish of the top-set path) where its
+// scratch fits; 0 selects top_set_finish everywhere (A/B builds)
+#ifndef HYG_TSF1
+#define HYG_TSF1 1
 #endif
 template <int NT>
 constexpr int kSortWaves = (NT / 64 < HYG_SORT_WAVES) ? NT / 64 : HYG_SORT_WAVES;
@@ -1116,6 +1124,7 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
       hyg_u192 tau = hyg_u192_zero();
       if (lane < L) tau = hyg_u192_add(preK, hyg_ceil_mul_f32_bf(((float)lane + Usys) / (float)L, Rr));
       const hyg_u192 tlast = rdlane192(tau, L > 0 ? L - 1 : 0);
+      TPH(31);
       if (L > 0 && hasB && !hyg_u192_ge(massA, tlast)) {
         status = FAST_FALLBACK_REGEN;
       } else {
@@ -1128,7 +1137,188 @@ __device__ __forceinline__ int top_set_finish(uint64_t* srt, int nA, bool hasB, 
           }
           parents[bb + lane] = key_index(srt[lo]);
         }
+        TPH(34);
       }
+    }
+    if (lane == 0) {
+      sh.Kk = bb;
+      sh.log_c = lc;
+      sh.fast = status;
+    }
+    TPH(33);
+    serial_end();
+  }
+  lds_barrier();
+  TPH(29);
+  return sh.fast;
+}
+
+// u192 -> f64 to within a few ulp (a search estimate only: every decision it
+// guides is checked exactly); the scale 2^-149 cancels in the ratios it forms
+__device__ __forceinline__ double u192_approx(const hyg_u192& a) {
+  auto w = [](uint64_t x) { return fma((double)(uint32_t)(x >> 32), 0x1p32, (double)(uint32_t)x); };
+  return fma(w(a.w2), 0x1p128, fma(w(a.w1), 0x1p64, w(a.w0)));
+}
+
+// #{j in [0, L) : ceil(T_j R) <= v} for the systematic targets
+// T_j = ((float)j + U) / (float)L (f32, as resampling_functions.py:58-67 forms
+// them; Ttab[j] holds T_j): T_j R <= v is T_j <= v / R. The estimate
+// j ~ (v / R) L - U is within 1e-5 of the exact threshold (T_j carries two f32
+// roundings, v / R here a relative error below 2^-49), so every j <= j0 - 2
+// counts and no j >= j0 + 2 does; the three candidates in between are
+// compared in f64 with a 2^-46 guard band and, inside it, exactly in integers.
+__device__ __forceinline__ int sys_count(const hyg_u192& v, const hyg_u192& R, double invR, int L, float U,
+                                         const float* Ttab) {
+  const double y = u192_approx(v) * invR;
+  double jf = y * (double)L - (double)U;
+  jf = jf < -1.0 ? -1.0 : (jf > (double)L ? (double)L : jf);
+  const int j0 = (int)floor(jf);
+  const double ylo = y * (1.0 - 0x1p-46), yhi = y * (1.0 + 0x1p-46);
+  float T[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {  // loads first (one LDS round trip)
+    const int j = j0 - 1 + k;
+    T[k] = Ttab[j < 0 ? 0 : (j >= L ? L - 1 : j)];
+  }
+  int c = j0 - 1 > 0 ? j0 - 1 : 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int j = j0 - 1 + k;
+    const double t = (double)T[k];
+    bool le = t < ylo;
+    if (!le && !(t > yhi) && j >= 0 && j < L) le = hyg_u192_ge(v, hyg_ceil_mul_f32_bf(T[k], R));  // exact
+    c += (le && j >= 0 && j < L) ? 1 : 0;
+  }
+  return c;
+}
+
+// The value of the lane below (lane 0: `first`), DPP wave_shr:1.
+__device__ __forceinline__ int wave_shr1(int v, int first) {
+  return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false);
+}
+
+// LDS bytes of top_set_finish1's scratch: the sort's two exchange buffers,
+// then the sorted masses' in-wave inclusive prefixes, then the targets T_j
+template <int NSW>
+constexpr size_t tsf1_bytes() { return 2 * 64 * NSW * sizeof(uint64_t) + 64 * NSW * sizeof(hyg_u192) + 64 * sizeof(float); }
+
+// top_set_finish for one key per lane (sorter wave w, lane l: sorted position
+// 64 w + l), shaped for latency: after the sort each sorting wave scans its
+// own masses and publishes its total (one barrier, no block scan); wave 0 then
+// runs the K loop on its own prefixes and finds the systematic targets by
+// counting them per sorted position (sys_count), 64 positions per pass, from
+// the first kept position on, instead of a binary search per target. Same
+// parents, Kk, log c and fallback decisions as top_set_finish.
+template <int NT, int NSW>
+__device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB, int N, int M, int cnt_fin,
+                                               const hyg_u192& massB, unsigned char* scr, int* parents, Shared& sh,
+                                               const ConstLds& cl, unsigned char* red, float Usys,
+                                               unsigned long long* ph, bool timed) {
+  static_assert(NSW <= NT / 64 && NSW <= 4, "sorting waves");
+  const int lane = lane_id();
+  const bool sorter = (NSW == NT / 64) || wave_id() < NSW;  // wave-uniform
+  const int base = (int)(threadIdx.x >> 6) * 64 + lane;
+  hyg_u192* preL = (hyg_u192*)(scr + 2 * 64 * NSW * sizeof(uint64_t));  // past the sort buffers
+  hyg_u192* wtot = (hyg_u192*)red;  // red's last readers are behind this step's barriers
+  uint64_t e[1];
+  hyg_u192 f = hyg_u192_zero(), inc = hyg_u192_zero();
+  if (sorter) {
+    e[0] = (base < nA) ? srt[base] : ~0ull;
+    int ib = 0;
+    Bitonic<64 * NSW, 1, 2, 1>::run(e, (uint64_t*)scr, ib);
+    TPH(27);
+    // (every wave loaded its keys before the first cross-wave barrier)
+    srt[base] = e[0];
+    const float m = hyg_expf(key_value(e[0]));
+    f = hyg_fix149f((base < nA) ? m : 0.0f);
+    inc = wave_incl192(f);
+    preL[base] = inc;
+    if (lane == 63) wtot[wave_id()] = inc;
+  } else {
+    constexpr int nb = bitonic_lds_stages(64 * NSW, 1);
+#pragma unroll
+    for (int i = 0; i < nb; ++i) lds_barrier();
+    e[0] = ~0ull;
+  }
+  lds_barrier();
+  TPH(28);
+  if (wave_id() == 0) {
+    serial_begin();
+    hyg_u192 massA = hyg_u192_zero();
+#pragma unroll
+    for (int w = 0; w < NSW; ++w) massA = hyg_u192_add(massA, wtot[w]);
+    const hyg_u192 total = hyg_u192_add(massA, massB);  // every significant weight's mass
+    // lane a: c(a) (loop-variable semantics of :12-31) from the suffix mass
+    // total - C(a - 1), C(a - 1) = this lane's exclusive prefix
+    const int a = lane;
+    const float xk = key_value(e[0]);
+    const int cap = nA < M ? nA : M;
+    const uint64_t capmask = (cap >= 64) ? ~0ull : ((1ull << cap) - 1ull);
+    int flag = 0;
+    float ca = 0.0f;
+    hyg_u192 rva = hyg_u192_zero();
+    if (a < M && a < N) {
+      if (a <= nA) rva = hyg_u192_sub(total, hyg_u192_sub(inc, f));
+      else if (hasB) flag = 1;  // prefix outside A
+      const double rvd = hyg_u192_to_f64(rva);
+      const float l2 = (rvd == 0.0) ? HYG_NINFF : (float)hyg_log(rvd);
+      ca = cl.logMa[a] - l2;
+    }
+    TPH(30);
+    int aa = 0, bb = -1, ovf = 0;
+    while (aa != bb && aa < N && aa < M) {
+      const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), aa));
+      int nxt = 0;
+      if (hyg_isfinitef(c)) {  // uniform
+        nxt = (int)__builtin_popcountll(wave_ballot((float)(c + xk) > 0.0f) & capmask);
+        if (nxt == nA && nA < M && hasB) ovf = 1;  // the count may continue below A
+      } else if (c > 0.0f) {
+        nxt = cnt_fin;  // +inf: every finite particle
+      }
+      ovf |= __builtin_amdgcn_readlane(flag, aa);
+      bb = aa;
+      aa = nxt > aa ? nxt : aa;
+    }
+    TPH(32);
+    const float lc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ca), bb));
+    int status = FAST_DONE;
+    if (ovf) {
+      status = FAST_FALLBACK_REGEN;
+    } else if (bb < N && hyg_isfinitef(lc)) {
+      // (bb < nA here: bb > nA sets ovf, and bb = nA leaves a zero residual
+      // mass when nothing lies outside A, so log c is infinite)
+      if (lane < bb) parents[lane] = key_index(e[0]);
+      const int L = M - bb;
+      TPH(31);
+      if (L > 0) {
+        // systematic residual (:32-40, :56-69): target j lands on the first
+        // sorted position p >= K with C(p) >= preK + ceil(T_j R); position p
+        // takes the targets j in [count(C(p - 1)), count(C(p)))
+        const hyg_u192 Rr = rdlane192(rva, bb);
+        const double invR = 1.0 / u192_approx(Rr);
+        const hyg_u192 preK = hyg_u192_sub(total, Rr);
+        float* Ttab = (float*)(scr + tsf1_bytes<NSW>() - 64 * sizeof(float));
+        if (lane < L) Ttab[lane] = ((float)lane + Usys) / (float)L;
+        wave_lds_sync();
+        int cprev = 0;
+        hyg_u192 cbase = hyg_u192_zero();  // C at the end of the chunks before
+#pragma unroll
+        for (int ci = 0; ci < NSW; ++ci) {
+          if (ci > 0) cbase = hyg_u192_add(cbase, wtot[ci - 1]);
+          if (64 * ci >= nA || cprev >= L) break;  // uniform (bb < M <= 64: chunk 0 holds it)
+          const int p = 64 * ci + lane;
+          const int pc = p < nA ? p : nA - 1;  // past A: the count of its last position
+          const hyg_u192 C = hyg_u192_add(cbase, preL[pc]);
+          const uint64_t key = srt[pc];
+          const int cnt = (p >= bb) ? sys_count(hyg_u192_sub(C, preK), Rr, invR, L, Usys, Ttab) : 0;
+          const int cex = wave_shr1(cnt, cprev);
+          for (int j = cex; j < cnt; ++j) parents[bb + j] = key_index(key);
+          cprev = __builtin_amdgcn_readlane(cnt, 63);
+        }
+        // targets past A: only when weights lie outside it
+        if (cprev < L) status = FAST_FALLBACK_REGEN;
+      }
+      TPH(34);
     }
     if (lane == 0) {
       sh.Kk = bb;
@@ -1243,8 +1433,15 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
   hyg_u192 massB = hyg_u192_zero();
   if (hasB) massB = sum_waves192<NW>(part_tot);
   TPH(26);
-  if (nA <= 64 * NSW)
+  if (nA <= 64 * NSW) {
+#if HYG_TSF1
+    if constexpr (NSW <= 4)
+      if (scr_bytes >= tsf1_bytes<NSW>())
+        return top_set_finish1<NT, NSW>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph,
+                                        timed);
+#endif
     return top_set_finish<NT, NSW, 1>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
+  }
   return top_set_finish<NT, NSW, 2>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
 }
 #undef TPH
@@ -2072,9 +2269,12 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             int* cn;
             if (segp) {
               // list position `lane` lies in the segment whose inclusive end
-              // is the first one above it
+              // is the first one above it (lanes q >= nseg hold the total L:
+              // every valid lane is below it, so all kSeg ends are read, each
+              // from a constant lane)
               int seg = 0, base = 0;
-              for (int q = 0; q < nseg; ++q) {
+#pragma unroll
+              for (int q = 0; q < kSeg; ++q) {
                 const int iv = __builtin_amdgcn_readlane(seg_incl, q);
                 seg += (iv <= lane) ? 1 : 0;
                 base = (iv <= lane) ? iv : base;
@@ -2098,15 +2298,20 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
               cdfa = (hyg_u128*)(Lg + 64);  // behind the 64 list logits
               cn = lst_n;
             }
+            BPH(12);
             const double lmax = wave_max(sv);
+            BPH(13);
             hyg_u128 ms = hyg_u128_zero();
             if (v) ms = hyg_exp_fix100(sv - lmax);
+            BPH(14);
             const hyg_u128 cdf = wave_incl128(ms);
+            BPH(15);
             hyg_u128 total;
             total.lo = rdlane64(cdf.lo, L - 1);
             total.hi = rdlane64(cdf.hi, L - 1);
             if (v) cdfa[lane] = cdf;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+            BPH(16);
             // lane b draws for trajectory b: first list entry with cdf > target
             if (lane < B && grp[lane] == g) {
               const uint64_t bits = pre_bits ? rb[(t & 1) * rbs + lane] : rnd(lane);  // = hyg_rand64(.., t, lane)
@@ -2467,7 +2672,8 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
     const double opt = steps - tot[10];
     fprintf(stderr, " | topset: compact=%.0f mass=%.0f gatherA=%.0f sort=%.0f prefix=%.0f kloop_sys=%.0f",
             tot[24] / opt, tot[25] / opt, tot[26] / opt, tot[27] / opt, tot[28] / opt, tot[29] / opt);
-    fprintf(stderr, " | kloop_sys split: c(a)=%.0f loop=%.0f systematic=%.0f", tot[30] / opt, tot[32] / opt,
+    fprintf(stderr, " | kloop_sys split: c(a)=%.0f loop=%.0f systematic=%.0f (targets=%.0f search=%.0f tail=%.0f)",
+            tot[30] / opt, tot[32] / opt, tot[31] / opt + tot[34] / opt + tot[33] / opt, tot[31] / opt, tot[34] / opt,
             tot[33] / opt);
     fprintf(stderr, " | per optimal step: topset=%.0f fallbacks=%.4f | per fallback: hist=%.0f bscan=%.0f scatter=%.0f "
             "bsort=%.0f scan=%.0f kloop=%.0f systematic=%.0f\n", tot[20] / opt, tot[21] / opt,
@@ -2512,8 +2718,10 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
       fprintf(stderr, " %s=%.0f", nm[k], tot[k] / steps);
       sum += tot[k] / steps;
     }
-    fprintf(stderr, " total(+tail)=%.0f | groups/step=%.2f finite logits/group=%.1f\n", sum, tot[10] / steps,
+    fprintf(stderr, " total(+tail)=%.0f | groups/step=%.2f finite logits/group=%.1f", sum, tot[10] / steps,
             (double)(tot[11] & 0xffffffffull) / (tot[10] > 0 ? (double)tot[10] : 1.0));
+    fprintf(stderr, " | wave0 split: entries=%.0f max=%.0f exp=%.0f scan=%.0f total=%.0f draw=%.0f\n", tot[12] / steps,
+            tot[13] / steps, tot[14] / steps, tot[15] / steps, tot[16] / steps, tot[4] / steps);
   }
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }
