@@ -312,8 +312,11 @@ constexpr int kNCut = 8;       // log-weight cutoffs of the top-set resampling p
 #ifndef HYG_LR256
 #define HYG_LR256 4
 #endif
+#ifndef HYG_LR512
+#define HYG_LR512 2
+#endif
 template <int NT>
-constexpr int kLRof = NT >= 512 ? 2 : HYG_LR256;
+constexpr int kLRof = NT >= 768 ? 2 : (NT >= 512 ? HYG_LR512 : HYG_LR256);
 // waves that sort the top set A: at most 256 keys (one per lane of 4 waves)
 // whatever the workgroup size, so a 512- or 1024-thread chain sorts no more
 // keys than a 256-thread one (HYG_SORT_WAVES overrides, for tuning builds)
@@ -1164,9 +1167,10 @@ __device__ __forceinline__ double u192_approx(const hyg_u192& a) {
 // T_j = ((float)j + U) / (float)L (f32, as resampling_functions.py:58-67 forms
 // them; Ttab[j] holds T_j): T_j R <= v is T_j <= v / R. The estimate
 // j ~ (v / R) L - U is within 1e-5 of the exact threshold (T_j carries two f32
-// roundings, v / R here a relative error below 2^-49), so every j <= j0 - 2
-// counts and no j >= j0 + 2 does; the three candidates in between are
-// compared in f64 with a 2^-46 guard band and, inside it, exactly in integers.
+// roundings, v / R here a relative error below 2^-49), so every j < j0 counts
+// and no j >= j0 + 2 does (j0 = floor of the estimate); the two candidates in
+// between are compared in f64 with a 2^-46 guard band and, inside it, exactly
+// in integers.
 __device__ __forceinline__ int sys_count(const hyg_u192& v, const hyg_u192& R, double invR, int L, float U,
                                          const float* Ttab) {
   const double y = u192_approx(v) * invR;
@@ -1174,16 +1178,16 @@ __device__ __forceinline__ int sys_count(const hyg_u192& v, const hyg_u192& R, d
   jf = jf < -1.0 ? -1.0 : (jf > (double)L ? (double)L : jf);
   const int j0 = (int)floor(jf);
   const double ylo = y * (1.0 - 0x1p-46), yhi = y * (1.0 + 0x1p-46);
-  float T[3];
+  float T[2];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {  // loads first (one LDS round trip)
-    const int j = j0 - 1 + k;
+  for (int k = 0; k < 2; ++k) {  // loads first (one LDS round trip)
+    const int j = j0 + k;
     T[k] = Ttab[j < 0 ? 0 : (j >= L ? L - 1 : j)];
   }
-  int c = j0 - 1 > 0 ? j0 - 1 : 0;
+  int c = j0 > 0 ? j0 : 0;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int j = j0 - 1 + k;
+  for (int k = 0; k < 2; ++k) {
+    const int j = j0 + k;
     const double t = (double)T[k];
     bool le = t < ylo;
     if (!le && !(t > yhi) && j >= 0 && j < L) le = hyg_u192_ge(v, hyg_ceil_mul_f32_bf(T[k], R));  // exact
@@ -1209,12 +1213,43 @@ constexpr size_t tsf1_bytes() { return 2 * 64 * NSW * sizeof(uint64_t) + 64 * NS
 // counting them per sorted position (sys_count), 64 positions per pass, from
 // the first kept position on, instead of a binary search per target. Same
 // parents, Kk, log c and fallback decisions as top_set_finish.
-template <int NT, int NSW>
+// The outside masses of the lists, for top_set_finish1<.., SPLIT = true>:
+// the lists hold the outside log-weights (f32 bits, -inf inside A).
+struct ListsB {
+  const int* lst;        // wave w's list at lst[w * stride], part_cnt[w * kNCut + kNCut - 1] entries
+  int stride;
+  const int* part_cnt;
+  hyg_u192* part_tot;    // one partial per non-sorting wave
+  bool narrow;           // every outside mass below e^-20, <= kNarrowPerLane images per lane: u128 sums
+                         // (a lane sums up to 2 ceil(N / NT) images: two lists)
+};
+// Exact image sum of the f32 masses exp(lw) of list w (lane-strided, two
+// entries per lane in flight).
+__device__ __forceinline__ void list_mass(const ListsB& lb, int w, hyg_u128& n128, hyg_u192& m192) {
+  const int cnt = lb.part_cnt[w * kNCut + kNCut - 1];
+  const int* L = lb.lst + w * lb.stride;
+  const int lane = lane_id();
+  for (int b = 0; b < cnt; b += 128) {  // cnt is wave-uniform
+    const int i0 = b + lane, i1 = b + 64 + lane;
+    const float x0 = __builtin_bit_cast(float, L[i0 < cnt ? i0 : b]);
+    const float x1 = __builtin_bit_cast(float, L[i1 < cnt ? i1 : b]);
+    const float m0 = (i0 < cnt) ? hyg_expf(x0) : 0.0f, m1 = (i1 < cnt) ? hyg_expf(x1) : 0.0f;
+    if (lb.narrow) {
+      n128 = hyg_u128_add(n128, hyg_u128_add(hyg_fix149f_low128(m0), hyg_fix149f_low128(m1)));
+    } else {
+      m192 = hyg_u192_add(m192, hyg_u192_add(hyg_fix149f(m0), hyg_fix149f(m1)));
+    }
+  }
+}
+
+template <int NT, int NSW, bool SPLIT>
 __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB, int N, int M, int cnt_fin,
-                                               const hyg_u192& massB, unsigned char* scr, int* parents, Shared& sh,
-                                               const ConstLds& cl, unsigned char* red, float Usys,
-                                               unsigned long long* ph, bool timed) {
+                                               const hyg_u192& massB_in, unsigned char* scr, int* parents,
+                                               Shared& sh, const ConstLds& cl, unsigned char* red, float Usys,
+                                               const ListsB& lb, unsigned long long* ph, bool timed) {
   static_assert(NSW <= NT / 64 && NSW <= 4, "sorting waves");
+  constexpr int NW = NT / 64, NNS = NW - NSW;
+  static_assert(!SPLIT || NNS >= NSW, "the outside masses need idle waves");
   const int lane = lane_id();
   const bool sorter = (NSW == NT / 64) || wave_id() < NSW;  // wave-uniform
   const int base = (int)(threadIdx.x >> 6) * 64 + lane;
@@ -1235,9 +1270,24 @@ __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB,
     preL[base] = inc;
     if (lane == 63) wtot[wave_id()] = inc;
   } else {
+    // SPLIT: the waves that do not sort sum the outside masses meanwhile,
+    // wave NSW + v the lists v and v + NNS (NW <= 2 NNS): the first before the
+    // sort's first cross-wave barrier, the second after its last (both before
+    // the first barrier delay the sort: measured)
+    static_assert(!SPLIT || NW <= 2 * NNS, "two lists per idle wave");
     constexpr int nb = bitonic_lds_stages(64 * NSW, 1);
+    hyg_u128 n128 = hyg_u128_zero();
+    hyg_u192 m192 = hyg_u192_zero();
+    const int v = wave_id() - NSW;
+    if (SPLIT && hasB) list_mass(lb, v, n128, m192);  // uniform
 #pragma unroll
     for (int i = 0; i < nb; ++i) lds_barrier();
+    if (SPLIT && hasB) {
+      if (v + NNS < NW) list_mass(lb, v + NNS, n128, m192);
+      if (lb.narrow) { m192.w0 = n128.lo; m192.w1 = n128.hi; m192.w2 = 0; }
+      const hyg_u192 ws = wave_sum192(m192);
+      if (lane == 0) lb.part_tot[v] = ws;
+    }
     e[0] = ~0ull;
   }
   lds_barrier();
@@ -1247,6 +1297,11 @@ __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB,
     hyg_u192 massA = hyg_u192_zero();
 #pragma unroll
     for (int w = 0; w < NSW; ++w) massA = hyg_u192_add(massA, wtot[w]);
+    hyg_u192 massB = massB_in;
+    if (SPLIT && hasB) {
+#pragma unroll
+      for (int w = 0; w < NNS; ++w) massB = hyg_u192_add(massB, lb.part_tot[w]);
+    }
     const hyg_u192 total = hyg_u192_add(massA, massB);  // every significant weight's mass
     // lane a: c(a) (loop-variable semantics of :12-31) from the suffix mass
     // total - C(a - 1), C(a - 1) = this lane's exclusive prefix
@@ -1300,17 +1355,27 @@ __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB,
         float* Ttab = (float*)(scr + tsf1_bytes<NSW>() - 64 * sizeof(float));
         if (lane < L) Ttab[lane] = ((float)lane + Usys) / (float)L;
         wave_lds_sync();
-        int cprev = 0;
-        hyg_u192 cbase = hyg_u192_zero();  // C at the end of the chunks before
+        // C at the start of each sorting wave's positions
+        hyg_u192 wb[NSW];
+        wb[0] = hyg_u192_zero();
 #pragma unroll
-        for (int ci = 0; ci < NSW; ++ci) {
-          if (ci > 0) cbase = hyg_u192_add(cbase, wtot[ci - 1]);
-          if (64 * ci >= nA || cprev >= L) break;  // uniform (bb < M <= 64: chunk 0 holds it)
-          const int p = 64 * ci + lane;
+        for (int w = 1; w < NSW; ++w) wb[w] = hyg_u192_add(wb[w - 1], wtot[w - 1]);
+        int cprev = 0;
+        // 64 positions per pass from the first kept one on (the deepest
+        // target sits about 60 positions past it at C3: mostly one pass)
+#pragma unroll
+        for (int i = 0; i < NSW; ++i) {
+          const int p0 = bb + 64 * i;
+          if (p0 >= nA || cprev >= L) break;  // uniform
+          const int p = p0 + lane;
           const int pc = p < nA ? p : nA - 1;  // past A: the count of its last position
-          const hyg_u192 C = hyg_u192_add(cbase, preL[pc]);
+          const int wp = pc >> 6;
+          hyg_u192 C = preL[pc];
+#pragma unroll
+          for (int w = 1; w < NSW; ++w)
+            if (wp == w) C = hyg_u192_add(C, wb[w]);
           const uint64_t key = srt[pc];
-          const int cnt = (p >= bb) ? sys_count(hyg_u192_sub(C, preK), Rr, invR, L, Usys, Ttab) : 0;
+          const int cnt = sys_count(hyg_u192_sub(C, preK), Rr, invR, L, Usys, Ttab);
           const int cex = wave_shr1(cnt, cprev);
           for (int j = cex; j < cnt; ++j) parents[bb + j] = key_index(key);
           cprev = __builtin_amdgcn_readlane(cnt, 63);
@@ -1339,7 +1404,7 @@ __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB,
 // counts of the cutoff sets per wave (part_cnt) were published with the
 // candidate lists before the log-sum-exp reduction.
 template <int NT, int NSW>
-__device__ __forceinline__ int top_set_resample(const double* W, int N, double mx, double logS, const int* lst, int lb, int cw,
+__device__ __forceinline__ int top_set_resample(const double* W, int N, double mx, double logS, int* lst, int lb, int cw,
                                 unsigned char* scr, size_t scr_bytes, uint64_t* srt, size_t srt_bytes,
                                 const int* part_cnt, hyg_u192* part_tot, int* parents, Shared& sh,
                                 const ConstLds& cl, unsigned char* red, int M, int cnt_fin, float Usys,
@@ -1377,6 +1442,12 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
   // ceil(N / NT) <= 128 of them, below 2^127.2) a lane's images are formed and
   // summed as u128.
   const bool narrow = ks >= kNarrowCut && (N + NT - 1) / NT <= kNarrowPerLane;
+  // SPLIT (workgroups with at least as many idle waves as sorting ones): the
+  // lists take the outside log-weights back and the idle waves sum their
+  // masses during the sort (top_set_finish1)
+  constexpr int NNS = NW - NSW;
+  constexpr bool kSplitB = HYG_TSF1 && NSW <= 4 && NNS >= NSW;
+  const bool split = kSplitB && nA <= 64 * NSW && scr_bytes >= tsf1_bytes<NSW>();
   hyg_u192 mb = hyg_u192_zero(), mb2 = hyg_u192_zero();
   hyg_u128 nb = hyg_u128_zero(), nb2 = hyg_u128_zero();
   constexpr int kLR = kLRof<NT>;
@@ -1403,7 +1474,13 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
       if (inA[r]) srt[off + lanes_below(bal)] = sort_key(lw[r], nn[r]);
       off += (int)__builtin_popcountll(bal);
     }
-    if (hasB && narrow) {  // uniform; expf(lw) is 0 below sig_thresh
+    if (split) {
+      if (hasB) {
+#pragma unroll
+        for (int r = 0; r < kLR; ++r)
+          if (b + r * 64 + lane < cw) lst[lb + b + r * 64 + lane] = __builtin_bit_cast(int, outA[r] ? lw[r] : HYG_NINFF);
+      }
+    } else if (hasB && narrow) {  // uniform; expf(lw) is 0 below sig_thresh
 #pragma unroll
       for (int r = 0; r < kLR; ++r) {
         const float m = hyg_expf(lw[r]);
@@ -1417,6 +1494,20 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
         const hyg_u192 f = hyg_fix149f(outA[r] ? m : 0.0f);
         if (r & 1) mb2 = hyg_u192_add(mb2, f); else mb = hyg_u192_add(mb, f);
       }
+    }
+  }
+  if constexpr (kSplitB) {
+    if (split) {
+      lds_barrier();  // the keys of A and the lists' log-weights
+      TPH(26);
+      ListsB lbs;
+      lbs.lst = lst;
+      lbs.stride = ((N + NT - 1) / NT) * 64;
+      lbs.part_cnt = part_cnt;
+      lbs.part_tot = part_tot;
+      lbs.narrow = ks >= kNarrowCut && 2 * ((N + NT - 1) / NT) <= kNarrowPerLane;
+      return top_set_finish1<NT, NSW, kSplitB>(srt, nA, hasB, N, M, cnt_fin, hyg_u192_zero(), scr, parents, sh, cl,
+                                               red, Usys, lbs, ph, timed);
     }
   }
   if (hasB) {
@@ -1437,8 +1528,8 @@ __device__ __forceinline__ int top_set_resample(const double* W, int N, double m
 #if HYG_TSF1
     if constexpr (NSW <= 4)
       if (scr_bytes >= tsf1_bytes<NSW>())
-        return top_set_finish1<NT, NSW>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph,
-                                        timed);
+        return top_set_finish1<NT, NSW, false>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys,
+                                               ListsB{}, ph, timed);
 #endif
     return top_set_finish<NT, NSW, 1>(srt, nA, hasB, N, M, cnt_fin, massB, scr, parents, sh, cl, red, Usys, ph, timed);
   }
