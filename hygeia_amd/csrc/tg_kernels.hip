@@ -332,8 +332,8 @@ template <int NT>
 constexpr int kSortWaves = (NT / 64 < HYG_SORT_WAVES) ? NT / 64 : HYG_SORT_WAVES;
 
 struct Lay {  // byte offsets into the dynamic LDS (32-bit: one SGPR each in the kernels)
-  uint32_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, rb, red, sh,
-      total;
+  uint32_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, rb, xo, red,
+      sh, total;
   uint32_t bcnt_bytes;
   int npad, nkeys, nt;
   int topset_r;  // keys per lane of the top-set sort: A holds <= 64 * topset_r per wave
@@ -390,6 +390,7 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
     l.grp = o; o = align_up(o + sizeof(int) * B, 16);
     l.gst = o; o = align_up(o + sizeof(uint64_t) * B, 16);
     l.rb = o; o = align_up(o + 2 * sizeof(uint64_t) * ((B + 3) / 4) * 4, 16);  // draw bits, two steps
+    l.xo = o; o = align_up(o + 2 * sizeof(uint64_t) * B, 16);  // sampled states of two steps (deferred outputs)
   }
   l.red = o; o = align_up(o + 2 * 32 * (NT / 64), 16);  // two slots: the step's log-sum-exp has its own
   l.sh = o; o = align_up(o + sizeof(Shared), 16);
@@ -2090,8 +2091,41 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
   int* grp = (int*)(smem + lay.grp);
   uint64_t* gst = (uint64_t*)(smem + lay.gst);
   uint64_t* rb = (uint64_t*)(smem + lay.rb);
+  uint64_t* xo = (uint64_t*)(smem + lay.xo);
   unsigned char* red = smem + lay.red;
   Shared& sh = *(Shared*)(smem + lay.sh);
+  // Trajectories and test-function means of time tt
+  // (run_inference_two_groups.py:233-240, 294-314) from the states wave 0
+  // sampled (xo[tt & 1]), one wave, trajectory b on lane b (B <= 64). From 128
+  // threads on they are written by wave 1 during the next step's draw, off
+  // wave 0's serial path (deferred by one step; the state buffer is double).
+  constexpr int kOutWave = NT >= 128 ? 1 : 0;
+  auto write_outputs = [&](int tt) {
+    const int lane = lane_id();
+    const bool v = lane < B;
+    uint64_t x = 0;
+    if (v) {
+      x = xo[(tt & 1) * B + lane];
+      const size_t o = (size_t)(ch.out_begin + tt) * B + lane;
+      o_merged[o] = (int16_t)hyg_st_m(x);
+      o_control[2 * o + 0] = (int16_t)hyg_st_dc(x);
+      o_control[2 * o + 1] = (int16_t)hyg_st_rc(x);
+      o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
+      o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
+    }
+    int myc = __builtin_popcountll(__ballot(v && hyg_st_m(x) == 0));
+    for (int r = 0; r < K; ++r) {
+      const int cc = __builtin_popcountll(__ballot(v && hyg_st_rc(x) == r));
+      const int ck = __builtin_popcountll(__ballot(v && hyg_st_rk(x) == r));
+      myc = (lane == 1 + r) ? cc : ((lane == 1 + K + r) ? ck : myc);
+    }
+    if (lane < 2 * K + 1) {
+      const float vv = (float)myc / (float)B;
+      if (lane == 0) o_split[ch.out_begin + tt] = vv;
+      else o_regime[(size_t)(ch.out_begin + tt) * K2 + (lane - 1)] = vv;
+    }
+  };
+  int pend = -1;  // the time whose outputs are still to be written (B <= 64)
 
   const uint8_t* rec0 = ws + ch.ws_offset;
   const size_t rstride = record_bytes(M);
@@ -2415,12 +2449,19 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
               idx[lane] = cn[lo];
             }
             serial_end();
+          } else if (kOutWave > 0 && g == 0 && pend >= 0 && wave_id() == kOutWave) {
+            write_outputs(pend);
           }
+          if (kOutWave > 0 && g == 0) pend = -1;
           BPH(4);
           if (g + 1 < ng) lds_barrier();  // the next group's list reuses the areas wave 0 read
         } else {
           // ---- general case: logits of all N in index order (built in place of
           //      the weights), block categorical
+          if (kOutWave > 0 && g == 0 && pend >= 0) {
+            if (wave_id() == kOutWave) write_outputs(pend);
+            pend = -1;
+          }
           if (!w_ready) {
             lds_barrier();  // the list areas (= the W area) are reused below
             make_W();
@@ -2462,23 +2503,11 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         uint64_t x = 0;
         if (v) {
           x = state_of(idx[lane]);
-          const size_t o = (size_t)(ch.out_begin + t) * B + lane;
-          o_merged[o] = (int16_t)hyg_st_m(x);
-          o_control[2 * o + 0] = (int16_t)hyg_st_dc(x);
-          o_control[2 * o + 1] = (int16_t)hyg_st_rc(x);
-          o_case[2 * o + 0] = (int16_t)hyg_st_dk(x);
-          o_case[2 * o + 1] = (int16_t)hyg_st_rk(x);
+          xo[(t & 1) * B + lane] = x;
         }
-        int myc = __builtin_popcountll(__ballot(v && hyg_st_m(x) == 0));
-        for (int r = 0; r < K; ++r) {
-          const int cc = __builtin_popcountll(__ballot(v && hyg_st_rc(x) == r));
-          const int ck = __builtin_popcountll(__ballot(v && hyg_st_rk(x) == r));
-          myc = (lane == 1 + r) ? cc : ((lane == 1 + K + r) ? ck : myc);
-        }
-        if (lane < 2 * K + 1) {
-          const float vv = (float)myc / (float)B;
-          if (lane == 0) o_split[ch.out_begin + t] = vv;
-          else o_regime[(size_t)(ch.out_begin + t) * K2 + (lane - 1)] = vv;
+        if constexpr (kOutWave == 0) {
+          wave_lds_sync();
+          write_outputs(t);
         }
         BPH(6);
         if (t > 0) {
@@ -2546,12 +2575,14 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       }
     }
     lds_barrier();
+    if (kOutWave > 0 && B <= 64) pend = t;
     s = s1;
     st1 = st2;
     w1 = w2;
     s1 = s2;
   }
   lds_barrier();
+  if (kOutWave > 0 && B <= 64 && pend >= 0 && wave_id() == kOutWave) write_outputs(pend);
   if (tid == 0 && status_out) status_out[blockIdx.x] = sh.status;
   if (dbg && tid == 0) {
     for (int k = 0; k < kPh - 1; ++k) dbg[(size_t)blockIdx.x * kPh + k] = ph_acc[k];
