@@ -2333,10 +2333,11 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
                     ark = hyg_st_rk(par);
           Pf3 pa{};
           if (act) pa = PF[lane];
-          for (int part = 0; part < 2; ++part) {
-            const int sa = part ? r1a : r0a, sb = part ? r1b : r0b;
-            for (int sl = sa + wv; sl < sb; sl += NW) {
-              const int sgv = part ? nseg0 + (sl - r1a) : (sl - r0a);  // segment of slot sl
+          // the reachable slots, both ranges, round-robin over the waves (one
+          // slot per wave from 8 waves on at d_c >= 3)
+          {
+            for (int sgv = wv; sgv < nseg; sgv += NW) {  // sgv: segment of slot sl
+              const int sl = (sgv < nseg0) ? r0a + sgv : r1a + (sgv - nseg0);
               const Child x = child_of(cl, K, am, adc, arc, adk, ark, pa, sl);
               const bool poss = act && trans_possible(cl.u, x, mn, dcn, rcn, dkn, rkn);
               if (__ballot(poss) == 0) {  // nothing in this slot reaches xn
