@@ -377,8 +377,10 @@ def main():
     workload = (f"{cfg_name} two_group {args.sites} CpG (22 chromosomes, 100k segments + 5k buffers), "
                 f"{args.samples}+{args.samples} samples, K={K}, M={M}, B={B}, "
                 f"{job_seeds(args)} seeds in total, chains sharded over the GPUs (LPT)")
-    tr = pmc_record("traffic", workload) if world == 1 else None
-    iss = pmc_record("issue", workload) if world == 1 else None
+    # (the PMC records hold whole-job launches: none for a rank's share)
+    whole = world == 1 and not args.shard
+    tr = pmc_record("traffic", workload) if whole else None
+    iss = pmc_record("issue", workload) if whole else None
     roof = {"bound": "hbm", "kernel": names[dom], "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": tr.get(names[dom]) if tr else None,
             "bytes_per_unit": bpu, "units_per_launch": units,

@@ -1882,7 +1882,9 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
         h.lrc = hc.x; h.l1c = hc.y; h.lrk = hk.x; h.l1k = hk.y;
       }
       // the weight of candidate n of step t-1, recomputed (the W area may hold
-      // the sort): weight_at's arithmetic with the child formed once
+      // the sort): weight_at's arithmetic with the child formed once. (Reading
+      // W[n] instead, with the top-set scratch moved out of the W area at 512
+      // threads, measured 0.8 % slower: r03r.)
       double w;
       if (prev_mode == MODE_INIT) {
         const int i = n / K, j = n - (n / K) * K;
@@ -2332,7 +2334,13 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
           const int am = hyg_st_m(par), adc = hyg_st_dc(par), arc = hyg_st_rc(par), adk = hyg_st_dk(par),
                     ark = hyg_st_rk(par);
           Pf3 pa{};
-          if (act) pa = PF[lane];
+          Hz4 hanc{};
+          double pwa = 0.0;
+          if (act) {  // the ancestor's rows, once per group (not per slot)
+            pa = PF[lane];
+            hanc = PHZ[lane];
+            pwa = PW[lane];
+          }
           // the reachable slots, both ranges, round-robin over the waves (one
           // slot per wave from 8 waves on at d_c >= 3)
           {
@@ -2346,7 +2354,21 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
               }
               double l = HYG_NINF;
               if (poss) {
-                const double w = weight_at(cl, K, lane, sl, s.mode, s.log_c, s.lse, P, PW, PHZ, Et);
+                // weight_at with the ancestor in registers and the child from
+                // child_of (the same state as tg_xi): same operands, same order
+                const uint64_t xs = hyg_st_pack(x.m, x.dc, x.rc, x.dk, x.rk);
+                const double tr = tg_trans_sel(cl.lPm[am * 2 + x.m], cl.lPc[arc * K + x.rc], cl.lU1, cl.lU2, cl.u,
+                                               am, adc, arc, adk, ark, xs, hanc);
+                double w = HYG_NINF;
+                if (hyg_isfinite(tr)) {
+                  const double lg = tr + (Et[x.rc] + Et[K + x.rk]);
+                  if (s.mode == MODE_KEEP) w = pwa + lg;
+                  else if (s.mode == MODE_UNBIASED) w = (-cl.log_M + s.lse) + lg;
+                  else {
+                    const double vv = (double)s.log_c + (pwa - s.lse);
+                    w = (pwa + lg) - (vv < 0.0 ? vv : 0.0);
+                  }
+                }
                 if (w > HYG_NINF) {
                   const double f = tg_trans_sel(cl.lPm[x.m * 2 + mn], cl.lPc[x.rc * K + rcn], cl.lU1, cl.lU2,
                                                 cl.u, x.m, x.dc, x.rc, x.dk, x.rk, xn, x.h);
