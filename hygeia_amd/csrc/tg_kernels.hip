@@ -2160,16 +2160,23 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     phz[o0] = h;
     pf[o0] = prefetch_rows(md, K, st);
   }
+  // The record pipeline of the steps below (the reads of records t-1 / t-2,
+  // the hazard rows of record t-1's ancestors and its LDS store) is the last
+  // wave's work when M <= 64, ancestor a on its lane a: that wave has no slot
+  // of its own in the list phase at 8 waves (d_c >= 3: K + 1 slots), so the
+  // loads leave the waves whose list work the draw waits for. Otherwise thread
+  // a holds ancestor a.
+  const int ra = (M <= 64 && NT >= 128) ? ((wave_id() == NT / 64 - 1) ? lane_id() : M) : tid;
   // stage-1 registers: record t-1
   StepScalars s1{};
   uint64_t st1 = 0;
   double w1 = 0.0;
   if (T >= 2) {
     s1 = *(const StepScalars*)rec_ptr(T - 2);
-    if (tid < M) {
+    if (ra < M) {
       const uint64_t* rst = (const uint64_t*)(rec_ptr(T - 2) + sizeof(StepScalars));
-      st1 = rst[tid];
-      w1 = ((const double*)(rst + M))[tid];
+      st1 = rst[ra];
+      w1 = ((const double*)(rst + M))[ra];
     }
   }
   {
@@ -2209,7 +2216,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     // ---- hazard rows of record t-1's ancestors (arrived: read during step t+1)
     double2 h1c = make_double2(0.0, 0.0), h1k = make_double2(0.0, 0.0);
     Pf3 pf1;
-    const bool have1 = (t > 0) && (tid < s1.n_par);
+    const bool have1 = (t > 0) && (ra < s1.n_par);
     if (have1) {
       h1c = hz_at(md, K, 0, hyg_st_rc(st1), hyg_st_dc(st1));
       h1k = hz_at(md, K, 1, hyg_st_rk(st1), hyg_st_dk(st1));
@@ -2222,10 +2229,10 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     if (t >= 2) {
       const uint8_t* rn = rec_ptr(t - 2);
       s2 = *(const StepScalars*)rn;
-      if (tid < M) {
+      if (ra < M) {
         const uint64_t* rst = (const uint64_t*)(rn + sizeof(StepScalars));
-        st2 = rst[tid];
-        w2 = ((const double*)(rst + M))[tid];
+        st2 = rst[ra];
+        w2 = ((const double*)(rst + M))[ra];
       }
     }
     // ---- emission block t/EB - 2 into the half freed after this step's rows
@@ -2581,7 +2588,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     //      (step t+1) are behind this step's barriers; the emission block into
     //      the ring half whose rows this step no longer reads
     if (have1) {
-      const int o = (bt ^ 1) * M + tid;
+      const int o = (bt ^ 1) * M + ra;
       pst[o] = st1;
       pw[o] = w1;
       Hz4 h;
