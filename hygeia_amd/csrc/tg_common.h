@@ -38,6 +38,10 @@ struct StepScalars {
   double pad;
 };
 static_assert(sizeof(StepScalars) == 32, "record scalars");
+// (the backward kernel reads them as dwords: mode 0, n_par 1, log_c 2, r_ph 3, lse 4-5)
+static_assert(offsetof(StepScalars, n_par) == 4 && offsetof(StepScalars, log_c) == 8 &&
+                  offsetof(StepScalars, r_ph) == 12 && offsetof(StepScalars, lse) == 16,
+              "record scalar dwords");
 
 #if defined(__HIPCC__)
 __host__ __device__

@@ -2222,13 +2222,16 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
       h1k = hz_at(md, K, 1, hyg_st_rk(st1), hyg_st_dk(st1));
       pf1 = prefetch_rows(md, K, st1);
     }
-    // ---- issue the read of record t-2
-    StepScalars s2{};
+    // ---- issue the read of record t-2. Its scalars come in as a vector load
+    //      (lane i < 8: dword i) and are unpacked at the end of the step: a
+    //      scalar load shares lgkmcnt with LDS, so the step's first LDS wait
+    //      (or the spill of its SGPRs) waited out its trip to L2 on every wave.
+    uint32_t sv2 = 0;
     uint64_t st2 = 0;
     double w2 = 0.0;
     if (t >= 2) {
       const uint8_t* rn = rec_ptr(t - 2);
-      s2 = *(const StepScalars*)rn;
+      if (lane_id() < 8) sv2 = ((const uint32_t*)rn)[lane_id()];
       if (ra < M) {
         const uint64_t* rst = (const uint64_t*)(rn + sizeof(StepScalars));
         st2 = rst[ra];
@@ -2609,7 +2612,16 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     s = s1;
     st1 = st2;
     w1 = w2;
-    s1 = s2;
+    {
+      // (StepScalars: mode, n_par, log_c, r_ph, lse; zero before record 0)
+      s1.mode = __builtin_amdgcn_readlane((int)sv2, 0);
+      s1.n_par = __builtin_amdgcn_readlane((int)sv2, 1);
+      s1.log_c = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)sv2, 2));
+      s1.r_ph = __builtin_amdgcn_readlane((int)sv2, 3);
+      s1.lse = d_of(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sv2, 5) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)sv2, 4));
+      s1.pad = 0.0;
+    }
   }
   lds_barrier();
   if (kOutWave > 0 && B <= 64 && pend >= 0 && wave_id() == kOutWave) write_outputs(pend);
