@@ -12,8 +12,11 @@ namespace hyg {
 constexpr int kDefaultThreads = 256;     // forward workgroup size
 constexpr int kDefaultThreadsBwd = 256;  // backward workgroup size (HYG_THREADS[_FWD/_BWD] override)
 // forward / backward workgroup size when a launch has at most one chain per CU
-// (tg_kernels.hip threads_per_chain; HYG_LOWOCC_THREADS overrides the forward's)
+// (tg_kernels.hip threads_per_chain; HYG_LOWOCC_THREADS overrides both): the
+// backward's list phase keeps 12 waves busy (768: 546 vs 558 ms at 145 chains,
+// r03x), the forward is faster at 512 (1327 vs 1377 ms)
 constexpr int kLowOccThreads = 512;
+constexpr int kLowOccThreadsBwd = 768;
 constexpr int kEBlock = 8;     // emission rows staged in LDS per block of steps
 
 // Device-side chain descriptor (lives in the workspace header).

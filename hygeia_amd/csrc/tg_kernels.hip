@@ -2664,8 +2664,9 @@ int device_cus() {
 //    (K = 12, C5: 145 KB): 512 (forward) / 768 (backward), more waves on the
 //    CU's one chain;
 //  - at most one chain per CU (e.g. an 8-GPU rank of the C3 job, 73 chains):
-//    kLowOccThreads, whose extra waves shorten the parallel phases of each
-//    step of the sequential chain (HYG_LOWOCC_THREADS: 256, 512 or 768);
+//    kLowOccThreads (forward) / kLowOccThreadsBwd (backward), whose extra
+//    waves shorten the parallel phases of each step of the sequential chain
+//    (HYG_LOWOCC_THREADS: 256, 512 or 768 for both);
 //  - else 256, up to three chains per CU (<= 168 VGPRs: C3 on one GPU, 582
 //    chains; an 8-GPU rank of C4, 291). A 384-thread workgroup does not buy
 //    two chains per CU: its six waves land 2-2-1-1 on the SIMDs, so a second
@@ -2675,7 +2676,7 @@ bool valid_width(int x) { return x == 64 || x == 128 || x == 256 || x == 512 || 
 int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
   if (g_force_threads[backward ? 1 : 0]) return g_force_threads[backward ? 1 : 0];
   static int env[2] = {-1, -1};
-  static int lowocc = -1;
+  static int lowocc = -1;  // 0: the defaults kLowOccThreads / kLowOccThreadsBwd
   const int k = backward ? 1 : 0;
   if (env[k] < 0) {
     const char* v = getenv(backward ? "HYG_THREADS_BWD" : "HYG_THREADS_FWD");
@@ -2686,7 +2687,7 @@ int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
   if (lowocc < 0) {
     const char* v = getenv("HYG_LOWOCC_THREADS");
     const int x = v ? atoi(v) : 0;
-    lowocc = (x == 256 || x == 512 || x == 768) ? x : kLowOccThreads;
+    lowocc = (x == 256 || x == 512 || x == 768) ? x : 0;
   }
   if (env[k]) return env[k];
   const int def = backward ? kDefaultThreadsBwd : kDefaultThreads;
@@ -2695,7 +2696,7 @@ int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
   // faster than 512 in r03d; the forward is faster at 512)
   if (2 * lds > 160 * 1024) return backward ? 768 : 512;
   if (c.M > 64) return def;  // the wider kernels assume the pipeline's M <= 64 (one ancestor per lane)
-  if (n_chains <= device_cus()) return lowocc;
+  if (n_chains <= device_cus()) return lowocc ? lowocc : (backward ? kLowOccThreadsBwd : kLowOccThreads);
   return def;
 }
 }  // namespace

@@ -112,6 +112,8 @@ def lib():
         vp, i32, u64 = C.c_void_p, C.c_int32, C.c_uint64
         L.oracle_sg_chain.restype = i32
         L.oracle_sg_chain.argtypes = [C.POINTER(SgParams), vp, i32, u64, u64, vp, vp]
+        L.oracle_sg_chain_refstruct.restype = i32
+        L.oracle_sg_chain_refstruct.argtypes = [C.POINTER(SgParams), vp, vp, i32, i32, u64, u64, vp, vp]
         L.oracle_sg_chain_pe.restype = i32
         L.oracle_sg_chain_pe.argtypes = [C.POINTER(SgParams), C.POINTER(SgPeParams), vp, i32, u64, u64, vp, vp]
         L.oracle_sg_pe_hazard.restype = i32
@@ -164,6 +166,19 @@ def chain(p, E, seed=0, chain_id=0, want_nparts=False):
     if want_nparts:
         out["nparts"] = nparts
     return out
+
+
+def chain_refstruct(p, meth, tot, seed=0, chain_id=0):
+    """chain() with the emission evaluated from the counts at every use (the
+    reference's cost structure, sg_oracle.c:sg_em_ref): the same outputs."""
+    meth = np.ascontiguousarray(meth, np.uint16)
+    tot = np.ascontiguousarray(tot, np.uint16)
+    if meth.ndim == 1:
+        meth, tot = meth[:, None], tot[:, None]
+    T, S = tot.shape
+    probs = np.empty((T, p.n_regimes), np.float64)
+    rc = lib().oracle_sg_chain_refstruct(C.byref(p), _ptr(meth), _ptr(tot), S, T, seed, chain_id, _ptr(probs), None)
+    return {"status": rc, "regime_probs": probs}
 
 
 def hazard(p, r, n):

@@ -206,8 +206,36 @@ int64_t oracle_sg_optimal_steps = 0; /* capped steps resampled by the optimal sc
 
 /* One chain over T sites: E [T][K] emission table. Writes probs [T][K]
  * (the smoothed regime probabilities). Returns HYG_OK / HYG_ENUMERIC / HYG_ENOMEM. */
+/* The reference's structure of the emission (singleGroup.h:611-627 through
+ * misc.h:630-640, called from computeWeightsCp, Smc.h:563-573): every use
+ * evaluates the Beta-Binomial log-density from the counts, 9 lgamma per sample,
+ * the same expressions as the table of oracle_sg_emission (hyg_sg_bb_tables),
+ * so the value is bit-identical. Used by oracle_sg_chain_refstruct, the CPU
+ * baseline timed in the reference's cost structure. */
+typedef struct {
+  const uint16_t* meth;
+  const uint16_t* tot;
+  int S;
+} sg_refcounts;
+static double sg_em_ref(const hyg_sg_consts* c, const sg_refcounts* rc, int64_t t, int r) {
+  const double a = c->alpha[r], b = c->beta[r];
+  double e = 0.0;
+  for (int s = 0; s < rc->S; ++s) {
+    const int n = rc->tot[t * rc->S + s], y = rc->meth[t * rc->S + s];
+    if (y > n) return -INFINITY;
+    double term = (lgamma((double)n + 1.0) - lgamma((double)y + 1.0)) - lgamma((double)(n - y) + 1.0);
+    term = term + lgamma((double)y + a);
+    term = term + lgamma((double)(n - y) + b);
+    term = term - lgamma((double)n + a + b);
+    term = term + (lgamma(a + b) - lgamma(a) - lgamma(b));
+    e = e + term;
+  }
+  return e;
+}
+
 static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, const double* E, int T, uint64_t seed,
-                         uint64_t chain_id, double* probs, int32_t* nparts_out, double* theta_out) {
+                         uint64_t chain_id, double* probs, int32_t* nparts_out, double* theta_out,
+                         const sg_refcounts* rcnt) {
   if (T < 1 || T >= HYG_DMAX - 2) return HYG_EINVAL;
   sg_model mo;
   int rc = sgm_init(&mo, p, T + 1);
@@ -275,7 +303,7 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
   for (int n = 0; n < N; ++n) {
     dC[n] = 1;
     rC[n] = n;
-    lwC[n] = -c->log_K + E[n];
+    lwC[n] = -c->log_K + (rcnt ? sg_em_ref(c, rcnt, 0, n) : E[n]);
   }
   double logZ = lse(lwC, N);
   if (!(logZ > -INFINITY)) { rc = HYG_ENUMERIC; goto done; }
@@ -381,11 +409,12 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
         }
       }
       /* sampleParticlesCp (:504-522) + computeWeightsCp (:536-574) */
-      const double* Et = E + (size_t)t * K;
+      const double* Et = rcnt ? NULL : E + (size_t)t * K;
       for (int n = 0; n < M; ++n) {
         dC[n] = dP[anc[n]] + 1;
         rC[n] = rP[anc[n]];
-        lwC[n] = lwres[n] + (sg_trans(&mo, dC[n], rC[n], dP[anc[n]], rP[anc[n]]) + Et[rC[n]]);
+        const double gt = rcnt ? sg_em_ref(c, rcnt, t, rC[n]) : Et[rC[n]];
+        lwC[n] = lwres[n] + (sg_trans(&mo, dC[n], rC[n], dP[anc[n]], rP[anc[n]]) + gt);
       }
       /* evaluateBackwardKernels (:288-326): K_q(n) = normalise_n(W_prev[n] + log f((1,q) | n)).
        * log f((1,q) | (d_n, r_n)) = b_n + log P[r_n][q] (b_n: the hazard part, sg_bpart;
@@ -432,7 +461,15 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
             }
             const double inv = 1.0 / S;
             for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = (tmp2[n] * G[rP[n]]) * inv;
-            lwC[M + q] = (mq + hyg_log(S)) + Et[q];
+            double gq;
+            if (rcnt) {  /* the reference evaluates log g inside its loop over the previous particles */
+              volatile double sink = 0.0;
+              for (int n = 0; n < Np; ++n) sink = sg_em_ref(c, rcnt, t, q);
+              gq = sink;
+            } else {
+              gq = Et[q];
+            }
+            lwC[M + q] = (mq + hyg_log(S)) + gq;
           } else {
             for (int n = 0; n < Np; ++n) BK[q * Nmax + n] = 0.0;
             lwC[M + q] = -INFINITY;
@@ -563,12 +600,19 @@ pe_fail:
 
 int oracle_sg_chain(const hyg_sg_params* p, const double* E, int T, uint64_t seed, uint64_t chain_id,
                     double* probs, int32_t* nparts_out) {
-  return sg_chain_core(p, NULL, E, T, seed, chain_id, probs, nparts_out, NULL);
+  return sg_chain_core(p, NULL, E, T, seed, chain_id, probs, nparts_out, NULL, NULL);
+}
+/* oracle_sg_chain with the emission evaluated from the counts at every use
+ * (the reference's cost structure, sg_em_ref): the same outputs bit for bit */
+int oracle_sg_chain_refstruct(const hyg_sg_params* p, const uint16_t* meth, const uint16_t* tot, int S, int T,
+                              uint64_t seed, uint64_t chain_id, double* probs, int32_t* nparts_out) {
+  sg_refcounts rc = {meth, tot, S};
+  return sg_chain_core(p, NULL, NULL, T, seed, chain_id, probs, nparts_out, NULL, &rc);
 }
 /* theta_out [1 + (T - 1) / every][K^2] */
 int oracle_sg_chain_pe(const hyg_sg_params* p, const hyg_sg_pe_params* pe, const double* E, int T, uint64_t seed,
                        uint64_t chain_id, double* probs, double* theta_out) {
-  return sg_chain_core(p, pe, E, T, seed, chain_id, probs, NULL, theta_out);
+  return sg_chain_core(p, pe, E, T, seed, chain_id, probs, NULL, theta_out, NULL);
 }
 int oracle_sg_pe_hazard(const hyg_sg_params* p, const double* theta, int L, hyg_sgpe_row* rows, int32_t* Lr) {
   /* hazard rows of the estimation path for tests: rows [K][L] */

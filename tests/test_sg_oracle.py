@@ -293,3 +293,16 @@ def test_concurrent_chains_equal_sequential_runs():
     for a, b in zip(seq, par):
         assert a["status"] == b["status"] == 0
         np.testing.assert_array_equal(a["regime_probs"], b["regime_probs"])
+
+
+@pytest.mark.parametrize("S,Nmax", [(1, 250), (4, 250), (2, 30)])
+def test_reference_structure_variant_equals_oracle(sg, S, Nmax):
+    # the CPU baseline's variant evaluates the Beta-Binomial from the counts at
+    # every use (9 lgamma per sample, inside the loop over previous particles
+    # for the fresh ones, as computeWeightsCp does): the same chain, bit for bit
+    meth, tot, _, _, _ = _data(6, 700, S=S, seed=11 + S, cov=12.0)
+    p = sg.make_params(K=6, Nmax=Nmax)
+    a = sg.chain(p, sg.emission(p, meth, tot), seed=3, chain_id=4)
+    b = sg.chain_refstruct(p, meth, tot, seed=3, chain_id=4)
+    assert a["status"] == b["status"] == 0
+    assert np.array_equal(a["regime_probs"], b["regime_probs"], equal_nan=True)

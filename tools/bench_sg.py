@@ -51,27 +51,36 @@ def bytes_per_site(S: int, K: int) -> int:
     return 4 * S + 4 + 8 * K
 
 
-def cpu_baseline(meth, tot, chains, params, seconds, threads, pe=False):
+def cpu_baseline(meth, tot, chains, params, seconds, threads, pe=False, refstruct=False):
+    """Sites/s of the CPU restatement on `threads` threads over prefixes of the
+    chains, sized to about `seconds`. refstruct: the reference's cost structure
+    (oracle_sg_chain_refstruct: the Beta-Binomial from the counts at every use,
+    9 lgamma per sample, K x N_prev of them per step for the fresh particles as in
+    computeWeightsCp, Smc.h:563-573); else the optimised port (one
+    emission table per site)."""
     from oracle import sg_binding as sb
 
     p = sb.SgParams.from_buffer_copy(bytes(params))
     ope = sb.make_pe()
 
-    def run(E, seed, cid):
+    def run(sl, seed, cid):
+        if refstruct:
+            return sb.chain_refstruct(p, meth[sl], tot[sl], seed, cid)
+        E = sb.emission(p, meth[sl], tot[sl])
         return sb.chain_pe(p, ope, E, seed, cid) if pe else sb.chain(p, E, seed, cid)
 
     s0 = chains[0][0]
-    n_cal = 2000
+    n_cal = 300 if refstruct else 2000
     t0 = time.perf_counter()
-    run(sb.emission(p, meth[s0:s0 + n_cal], tot[s0:s0 + n_cal]), 0, 1)
+    run(slice(s0, s0 + n_cal), 0, 1)
     per_site = (time.perf_counter() - t0) / n_cal
-    n = int(max(2000, min(400000, seconds / per_site)))
+    n = int(max(n_cal, min(400000, seconds / per_site)))
+    n = min(n, min(c[1] for c in chains[:threads]))  # a prefix of every chain used
     res = [0] * threads
 
     def work(i):
         b = chains[i % len(chains)][0]
-        sl = slice(b, b + n)
-        out = run(sb.emission(p, meth[sl], tot[sl]), i, 7 + i)
+        out = run(slice(b, b + n), i, 7 + i)
         assert out["status"] == 0
         res[i] = n
 
@@ -82,9 +91,12 @@ def cpu_baseline(meth, tot, chains, params, seconds, threads, pe=False):
     for t in th:
         t.join()
     dt = time.perf_counter() - t0
+    what = ("oracle_sg_chain_refstruct (the reference's structure: Beta-Binomial from the counts at every use) "
+            if refstruct else "oracle/sg_oracle.c emission + ")
     return {"value": sum(res) / dt, "unit": "CpG-sites/s", "cores": threads, "kind": "port",
+            "variant": "reference structure" if refstruct else "optimised port",
             "sample": f"{threads} threads x {n}-site prefixes of the chromosome chains, each one "
-                      f"oracle/sg_oracle.c emission + SMC + online smoothing"
+                      f"{what}SMC + online smoothing"
                       f"{' + online parameter estimation' if pe else ''}; {sum(res)} sites in {dt:.1f} s"}
 
 
@@ -252,16 +264,25 @@ def main():
         dt_cpu = time.perf_counter() - t0
         assert out["status"] == 0
         line["cpu_baseline"] = {"value": args.sites / dt_cpu, "unit": "CpG-sites/s", "cores": 1, "kind": "port",
+                                "variant": "optimised port",
                                 "sample": f"the whole C1 chain ({args.sites} sites) in full: oracle/sg_oracle.c "
                                           f"emission + SMC + online smoothing, {dt_cpu:.1f} s",
                                 "host": bench.host_cpus()}
+        # and the reference's cost structure on one thread, a bounded prefix of the chain
+        line["cpu_baseline"]["reference_structure"] = cpu_baseline(mh, th, chains, p, args.cpu_seconds, 1,
+                                                                   refstruct=True)
     elif not args.no_cpu_baseline:
         import bench
 
         host = bench.host_cpus()
-        line["cpu_baseline"] = cpu_baseline(meth.cpu().numpy().view(np.uint16), tot.cpu().numpy().view(np.uint16),
-                                            chains, p, args.cpu_seconds,
-                                            args.cpu_threads or host["usable"], pe=pe is not None)
+        mh, th = meth.cpu().numpy().view(np.uint16), tot.cpu().numpy().view(np.uint16)
+        nth = args.cpu_threads or host["usable"]
+        if pe is None:
+            # headline: the reference's cost structure; the optimised port beside it
+            line["cpu_baseline"] = cpu_baseline(mh, th, chains, p, args.cpu_seconds, nth, refstruct=True)
+            line["cpu_baseline"]["optimised_port"] = cpu_baseline(mh, th, chains, p, args.cpu_seconds, nth)
+        else:
+            line["cpu_baseline"] = cpu_baseline(mh, th, chains, p, args.cpu_seconds, nth, pe=True)
         line["cpu_baseline"]["unit"] = line["unit"]
         line["cpu_baseline"]["host"] = host
     L.hyg_sg_model_destroy(h)
