@@ -1,3 +1,4 @@
+#define _DEFAULT_SOURCE 1 /* lgamma_r */
 /*
  * sg_oracle.c -- CPU oracle of the single-group engine (TEST INFRASTRUCTURE).
  *
@@ -217,17 +218,24 @@ typedef struct {
   const uint16_t* tot;
   int S;
 } sg_refcounts;
+/* lgamma_r: the same values as lgamma without its write of the global signgam,
+ * which made threads of the baseline contend for one cache line (the reference
+ * runs one process per chain, so its lgamma calls never share it) */
+static double lg_r(double x) {
+  int sg;
+  return lgamma_r(x, &sg);
+}
 static double sg_em_ref(const hyg_sg_consts* c, const sg_refcounts* rc, int64_t t, int r) {
   const double a = c->alpha[r], b = c->beta[r];
   double e = 0.0;
   for (int s = 0; s < rc->S; ++s) {
     const int n = rc->tot[t * rc->S + s], y = rc->meth[t * rc->S + s];
     if (y > n) return -INFINITY;
-    double term = (lgamma((double)n + 1.0) - lgamma((double)y + 1.0)) - lgamma((double)(n - y) + 1.0);
-    term = term + lgamma((double)y + a);
-    term = term + lgamma((double)(n - y) + b);
-    term = term - lgamma((double)n + a + b);
-    term = term + (lgamma(a + b) - lgamma(a) - lgamma(b));
+    double term = (lg_r((double)n + 1.0) - lg_r((double)y + 1.0)) - lg_r((double)(n - y) + 1.0);
+    term = term + lg_r((double)y + a);
+    term = term + lg_r((double)(n - y) + b);
+    term = term - lg_r((double)n + a + b);
+    term = term + (lg_r(a + b) - lg_r(a) - lg_r(b));
     e = e + term;
   }
   return e;
