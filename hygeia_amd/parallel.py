@@ -61,11 +61,12 @@ def posterior_counts(split_probs, regime_probs, B: int, rows_out, rows_site, n_s
     return counts
 
 
-def allreduce_counts(counts):
+def allreduce_counts(counts, always: bool = False):
     """Sum of the per-site counts over all ranks (in place); a no-op without an
-    initialised process group."""
+    initialised process group, and at world size 1 unless `always` (which runs
+    the collective anyway, e.g. to exercise RCCL on a one-GPU box)."""
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized() and (always or dist.get_world_size() > 1):
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
     return counts

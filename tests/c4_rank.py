@@ -1,9 +1,10 @@
 """One rank of bench.py's C4 job on the GPU (TEST INFRASTRUCTURE): its LPT
 shard of a fixed multi-seed job over a small genome, the chains through the HIP
 path (DeviceChains), per-site posterior counts on the device, summed over the
-ranks by torch.distributed ("gloo": several ranks may share one GPU).
+ranks by torch.distributed ("gloo": several ranks may share one GPU; "nccl" = RCCL,
+one rank per GPU, device tensors).
 
-    python tests/c4_rank.py --rank R --world W --port P --out counts.npz
+    python tests/c4_rank.py --rank R --world W --port P --out counts.npz [--backend nccl]
 
 Used by tests/test_gpu_c4_sharded.py, which starts the ranks as fresh
 processes before they touch the GPU."""
@@ -34,8 +35,9 @@ def job_args():
     return argparse.Namespace(job="c4", seeds=2, total_seeds=SEEDS)
 
 
-def rank_counts(rank: int, world: int):
-    """This rank's chains on the GPU -> (counts [N_SITES][1+2K] int32 on the CPU, units)."""
+def rank_counts(rank: int, world: int, on_device: bool = False):
+    """This rank's chains on the GPU -> (counts [N_SITES][1+2K] int32, on the CPU
+    unless on_device, units, chains, threads per chain)."""
     import torch
 
     import bench
@@ -65,7 +67,7 @@ def rank_counts(rank: int, world: int):
                                        torch.from_numpy(dst).to(dev), N_SITES)
     threads = int(__import__("hygeia_amd._lib", fromlist=["load"]).load().hyg_tg_threads_per_chain(
         model.handle, len(chains)))
-    return counts.cpu(), units, len(chains), threads
+    return (counts if on_device else counts.cpu()), units, len(chains), threads
 
 
 def oracle_counts():
@@ -108,6 +110,7 @@ def main():
     ap.add_argument("--world", type=int, required=True)
     ap.add_argument("--port", type=int, required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--backend", default="gloo", choices=("gloo", "nccl"))
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -116,15 +119,19 @@ def main():
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(a.port)
-    dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
+    nccl = a.backend == "nccl"
+    if nccl:  # RCCL: one rank per GPU, device tensors
+        torch.cuda.set_device(a.rank % torch.cuda.device_count())
+    dist.init_process_group(a.backend, rank=a.rank, world_size=a.world)
     try:
-        counts, units, n_chains, threads = rank_counts(a.rank, a.world)
-        parallel.allreduce_counts(counts)
-        uu = torch.tensor([units, n_chains], dtype=torch.int64)
+        counts, units, n_chains, threads = rank_counts(a.rank, a.world, on_device=nccl)
+        # (world 1: the same collective as bench.py's, through RCCL over this GPU)
+        parallel.allreduce_counts(counts, always=nccl)
+        uu = torch.tensor([units, n_chains], dtype=torch.int64, device=counts.device)
         dist.all_reduce(uu)
         if a.rank == 0:
-            np.savez(a.out, counts=counts.numpy(), units=int(uu[0].item()), chains=int(uu[1].item()),
-                     threads=threads)
+            np.savez(a.out, counts=counts.cpu().numpy(), units=int(uu[0].item()), chains=int(uu[1].item()),
+                     threads=threads, backend=a.backend)
     finally:
         dist.destroy_process_group()
 
