@@ -148,8 +148,29 @@ def chain_id(chrom: str, batch: int) -> int:
 
 
 def _read_matrix(path: str) -> np.ndarray:
+    """A whole-chromosome count matrix (run_inference_two_groups.py:177-191 reads
+    it with pd.read_table(sep=",", header=None)) as float64.
+
+    Parsed by pyarrow's multi-threaded CSV reader (about 2.7x pandas on a chr1
+    matrix, most of a single `hygeia infer` task's host time). The pipeline's
+    files hold integer counts (plain or '%.18e' text), which every correct
+    parser reads exactly, so the values equal pandas'; a matrix with any
+    non-integral or non-finite value (or one pyarrow cannot read) is re-read
+    with pandas, the reference's parser, so such input keeps its exact values."""
     import pandas as pd
 
+    try:
+        import pyarrow.csv as pacsv
+
+        tb = pacsv.read_csv(path, read_options=pacsv.ReadOptions(autogenerate_column_names=True),
+                            parse_options=pacsv.ParseOptions(delimiter=","))
+        cols = [c.to_numpy(zero_copy_only=False) for c in tb.columns]
+        if tb.num_columns > 0 and all(c.dtype.kind in "iuf" for c in cols):
+            a = np.column_stack(cols).astype(np.float64)
+            if np.all(np.isfinite(a)) and np.all(a == np.rint(a)) and np.all(np.abs(a) < 2.0 ** 53):
+                return a
+    except (ImportError, ValueError, OSError):  # pyarrow.lib.ArrowInvalid is a ValueError
+        pass
     return pd.read_csv(path, sep=",", header=None, dtype=np.float64).to_numpy()
 
 

@@ -147,3 +147,31 @@ def test_fast_savetxt_matches_numpy(tmp_path, shape, dtype):
     cli._savetxt(str(tmp_path / "c.csv"), a)
     np.savetxt(str(tmp_path / "d.csv"), a, delimiter=",")
     assert (tmp_path / "c.csv").read_bytes() == (tmp_path / "d.csv").read_bytes()
+
+
+def test_read_matrix_equals_pandas(tmp_path):
+    """cli._read_matrix (pyarrow, pandas re-read for non-integral input) gives
+    pandas' values (the reference's parser, run_inference_two_groups.py:177-191)
+    on plain and '%.18e' integer text, gzip or not, and on non-integral text."""
+    import pandas as pd
+
+    rng = np.random.default_rng(5)
+    a = rng.poisson(40, (3000, 3)).astype(np.int64)
+    cases = {
+        "plain.txt.gz": "\n".join(",".join(str(x) for x in r) for r in a) + "\n",
+        "sci.txt.gz": "\n".join(",".join("%.18e" % x for x in r) for r in a) + "\n",
+        "frac.txt": "0.1,2\n3.3333333333333333,1e-300\n",
+        "one.txt": "7\n",
+    }
+    for name, text in cases.items():
+        p = str(tmp_path / name)
+        if name.endswith(".gz"):
+            with gzip.open(p, "wt") as fh:
+                fh.write(text)
+        else:
+            with open(p, "w") as fh:
+                fh.write(text)
+        got = cli._read_matrix(p)
+        ref = pd.read_csv(p, sep=",", header=None, dtype=np.float64).to_numpy()
+        assert got.dtype == np.float64 and got.shape == ref.shape
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), name
