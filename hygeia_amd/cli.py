@@ -174,6 +174,20 @@ def _read_matrix(path: str) -> np.ndarray:
     return pd.read_csv(path, sep=",", header=None, dtype=np.float64).to_numpy()
 
 
+def _read_inputs(data_dir: str, chrom: str):
+    """positions, n_total_reads_control, n_methylated_reads_control,
+    n_total_reads_case, n_methylated_reads_case of one chromosome
+    (run_inference_two_groups.py:177-191), the five files read concurrently
+    (each file's gzip stream decompresses on one thread)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    names = ["positions", "n_total_reads_control", "n_methylated_reads_control", "n_total_reads_case",
+             "n_methylated_reads_case"]
+    paths = [os.path.join(data_dir, f"{n}_{chrom}.txt.gz") for n in names]
+    with ThreadPoolExecutor(max_workers=len(paths)) as ex:
+        return list(ex.map(_read_matrix, paths))
+
+
 def read_theta(single_group_dir: str, chrom: str) -> np.ndarray:
     """theta_{chrom}.csv.gz, column 'data' (run_inference_two_groups.py:76-79)."""
     import pandas as pd
@@ -234,12 +248,7 @@ def infer(argv: Sequence[str]) -> int:
     if theta.shape[0] != K * K:
         raise ValueError(f"theta_{chrom}.csv.gz holds {theta.shape[0]} values, expected K^2 = {K * K}")
 
-    dd = str(f["data_dir"])
-    positions = _read_matrix(os.path.join(dd, f"positions_{chrom}.txt.gz"))
-    tot_c = _read_matrix(os.path.join(dd, f"n_total_reads_control_{chrom}.txt.gz"))
-    meth_c = _read_matrix(os.path.join(dd, f"n_methylated_reads_control_{chrom}.txt.gz"))
-    tot_k = _read_matrix(os.path.join(dd, f"n_total_reads_case_{chrom}.txt.gz"))
-    meth_k = _read_matrix(os.path.join(dd, f"n_methylated_reads_case_{chrom}.txt.gz"))
+    positions, tot_c, meth_c, tot_k, meth_k = _read_inputs(str(f["data_dir"]), chrom)
 
     seg = segment_index(positions.shape[0], batch, int(f["segment_size"]), int(f["buffer_size"]))
     if seg is None:
@@ -326,12 +335,8 @@ def infer_many(argv: Sequence[str]) -> int:
     theta = read_theta(str(f["single_group_dir"]), chrom)
     if theta.shape[0] != K * K:
         raise ValueError(f"theta_{chrom}.csv.gz holds {theta.shape[0]} values, expected K^2 = {K * K}")
-    dd = str(f["data_dir"])
-    positions = _read_matrix(os.path.join(dd, f"positions_{chrom}.txt.gz"))
-    tot_c = _read_matrix(os.path.join(dd, f"n_total_reads_control_{chrom}.txt.gz")).astype(np.float32)
-    meth_c = _read_matrix(os.path.join(dd, f"n_methylated_reads_control_{chrom}.txt.gz")).astype(np.float32)
-    tot_k = _read_matrix(os.path.join(dd, f"n_total_reads_case_{chrom}.txt.gz")).astype(np.float32)
-    meth_k = _read_matrix(os.path.join(dd, f"n_methylated_reads_case_{chrom}.txt.gz")).astype(np.float32)
+    positions, tot_c, meth_c, tot_k, meth_k = _read_inputs(str(f["data_dir"]), chrom)
+    tot_c, meth_c, tot_k, meth_k = (a.astype(np.float32) for a in (tot_c, meth_c, tot_k, meth_k))
     n = positions.shape[0]
     batches = (list(range(0, n // S + 1)) if str(f["batches"]) == "all"
                else [int(x) for x in str(f["batches"]).split(",") if x != ""])
