@@ -262,37 +262,49 @@ def infer(argv: Sequence[str]) -> int:
         raise AssertionError("methylated reads exceed total reads")
     ret = slice(r0, r1)
 
-    _write_batch_inputs(path, ob_c, ob_k, nt_c, nt_k, pos, ret)
-
-    from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
+    from concurrent.futures import ThreadPoolExecutor
 
     T = hi - lo
     max_reads = int(max(nt_c.max(initial=0), nt_k.max(initial=0)))
     log_z: Dict[int, float] = {}
     times: Dict[int, float] = {}
-    for M in f["num_resampled_particles"]:
-        print(M)
-        N = int(M) * (2 * K + K * K)
-        model = two_group.CaseControlModel(
-            mu, sigma, theta, minimum_duration=int(f["minimum_duration"]), omega_case=float(f["omega_case"]),
-            merge_log_prob=float(f["merge_log_prob"]), split_prob=float(f["split_prob"]),
-            num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
-            max_total_reads=max_reads, max_duration=T + 1, multinomial=bool(f["multinomial"]))
-        t0 = time.time()
-        res, _final_w, ex = two_group.run({"control": ob_c, "case": ob_k}, {"control": nt_c, "case": nt_k}, model,
-                                          seed, chain_id(chrom, batch))
-        times[N] = time.time() - t0
-        log_z[N] = float(ex["log_z"])
-        pr = res.particle
-        np.savez_compressed(os.path.join(path, f"optimal_backward_particles_merged_state_{N}_{seed}"),
-                            pr["merged_state"].astype(np.int16)[ret])
-        np.savez_compressed(os.path.join(path, f"optimal_backward_particles_control_state_{N}_{seed}"),
-                            pr["control_state"].astype(np.int16)[ret])
-        np.savez_compressed(os.path.join(path, f"optimal_backward_particles_case_state_{N}_{seed}"),
-                            pr["case_state"].astype(np.int16)[ret])
-        np.savez_compressed(os.path.join(path, f"optimal_split_probs_{N}_{seed}"), ex["split_probs"])
-        np.savez_compressed(os.path.join(path, f"optimal_regime_probs_{N}_{seed}"), ex["regime_probs"])
-        model.close()
+    # The result files are written by a small pool (gzip / zlib release the GIL):
+    # the batch's input copies while the chain runs on the GPU, each run's
+    # arrays while the next one runs; every write is joined (and its error
+    # raised) before the timing files, as the reference writes those last.
+    with ThreadPoolExecutor(max_workers=5) as pool:
+        writes = _write_batch_inputs(path, ob_c, ob_k, nt_c, nt_k, pos, ret, pool)
+
+        from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
+
+        for M in f["num_resampled_particles"]:
+            print(M)
+            N = int(M) * (2 * K + K * K)
+            model = two_group.CaseControlModel(
+                mu, sigma, theta, minimum_duration=int(f["minimum_duration"]), omega_case=float(f["omega_case"]),
+                merge_log_prob=float(f["merge_log_prob"]), split_prob=float(f["split_prob"]),
+                num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
+                max_total_reads=max_reads, max_duration=T + 1, multinomial=bool(f["multinomial"]))
+            t0 = time.time()
+            try:
+                res, _final_w, ex = two_group.run({"control": ob_c, "case": ob_k}, {"control": nt_c, "case": nt_k},
+                                                  model, seed, chain_id(chrom, batch))
+            finally:
+                model.close()
+            times[N] = time.time() - t0
+            log_z[N] = float(ex["log_z"])
+            pr = res.particle
+            for name, arr in ((f"optimal_backward_particles_merged_state_{N}_{seed}",
+                               pr["merged_state"].astype(np.int16)[ret]),
+                              (f"optimal_backward_particles_control_state_{N}_{seed}",
+                               pr["control_state"].astype(np.int16)[ret]),
+                              (f"optimal_backward_particles_case_state_{N}_{seed}",
+                               pr["case_state"].astype(np.int16)[ret]),
+                              (f"optimal_split_probs_{N}_{seed}", ex["split_probs"]),
+                              (f"optimal_regime_probs_{N}_{seed}", ex["regime_probs"])):
+                writes.append(pool.submit(np.savez_compressed, os.path.join(path, name), arr))
+        for w in writes:
+            w.result()
     with open(os.path.join(path, f"log_normalizing_constants_optimal_{seed}.txt"), "w") as fh:
         print(log_z, file=fh)
     with open(os.path.join(path, f"optimal_time_{seed}.txt"), "w") as fh:
@@ -302,12 +314,19 @@ def infer(argv: Sequence[str]) -> int:
     return 0
 
 
-def _write_batch_inputs(path: str, ob_c, ob_k, nt_c, nt_k, pos, ret) -> None:
-    _savetxt(os.path.join(path, "observations_control.csv.gz"), ob_c.astype(np.int16)[ret])
-    _savetxt(os.path.join(path, "observations_case.csv.gz"), ob_k.astype(np.int16)[ret])
-    _savetxt(os.path.join(path, "n_total_reads_control.csv.gz"), nt_c.astype(np.int16)[ret])
-    _savetxt(os.path.join(path, "n_total_reads_case.csv.gz"), nt_k.astype(np.int16)[ret])
-    _savetxt(os.path.join(path, "positions.csv.gz"), pos[ret])
+def _write_batch_inputs(path: str, ob_c, ob_k, nt_c, nt_k, pos, ret, pool=None):
+    """The batch's input copies (run_inference_two_groups.py:246-254); with a
+    pool, submitted to it (returns the futures), else written here."""
+    jobs = [("observations_control.csv.gz", ob_c.astype(np.int16)[ret]),
+            ("observations_case.csv.gz", ob_k.astype(np.int16)[ret]),
+            ("n_total_reads_control.csv.gz", nt_c.astype(np.int16)[ret]),
+            ("n_total_reads_case.csv.gz", nt_k.astype(np.int16)[ret]),
+            ("positions.csv.gz", pos[ret])]
+    if pool is None:
+        for name, a in jobs:
+            _savetxt(os.path.join(path, name), a)
+        return []
+    return [pool.submit(_savetxt, os.path.join(path, name), a) for name, a in jobs]
 
 
 MANY_FLAGS = FLAGS_SPEC + [
