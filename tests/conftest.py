@@ -10,6 +10,11 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP (MI355X) device")
+    config.addinivalue_line("markers", "last: run after every other test (a failure under -x stops nothing else)")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=lambda it: it.get_closest_marker("last") is not None)  # stable: the rest keep their order
 
 
 @pytest.fixture(scope="session")

@@ -58,6 +58,7 @@ def test_c4_two_ranks_equal_one_rank_and_oracle(tmp_path):
     assert np.all(got["counts"][:, 1:1 + c4_rank.K].sum(1) == c4_rank.SEEDS * c4_rank.B)
 
 
+@pytest.mark.last
 @pytest.mark.timeout(600)
 def test_c4_rccl_collective_one_rank(tmp_path):
     """The product collective (parallel.allreduce_counts on device tensors)
