@@ -391,7 +391,9 @@ def main():
         roof["issue"] = {"valu_wave_instr_per_s": rate, "peak": N_SIMD * clk / VALU_ISSUE_CYCLES,
                          "clock_hz": clk, "frac": rate / (N_SIMD * clk / VALU_ISSUE_CYCLES),
                          "source": f"profiles/pmc_issue.json (SQ_INSTS_VALU, GRBM_GUI_ACTIVE; build {iss['source_hash']})"}
-    n_gpus = min(world, torch.cuda.device_count())  # a gloo rehearsal may put several ranks on one GPU
+    # one rank per GPU over RCCL (nccl: any number of nodes); only a gloo rehearsal
+    # may put several ranks on one node's GPUs
+    n_gpus = world if args.dist_backend == "nccl" or world == 1 else min(world, torch.cuda.device_count())
     line = {
         "metric": METRIC, "value": value, "unit": "CpG-sites*seeds/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,

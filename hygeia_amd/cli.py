@@ -169,8 +169,8 @@ def _read_matrix(path: str) -> np.ndarray:
             a = np.column_stack(cols).astype(np.float64)
             if np.all(np.isfinite(a)) and np.all(a == np.rint(a)) and np.all(np.abs(a) < 2.0 ** 53):
                 return a
-    except (ImportError, ValueError, OSError):  # pyarrow.lib.ArrowInvalid is a ValueError
-        pass
+    except Exception:  # noqa: BLE001 -- any pyarrow failure (ArrowInvalid, ArrowNotImplementedError,
+        pass  # ArrowTypeError, ...) falls back to pandas, the reference's parser
     return pd.read_csv(path, sep=",", header=None, dtype=np.float64).to_numpy()
 
 
@@ -275,34 +275,12 @@ def infer(argv: Sequence[str]) -> int:
     with ThreadPoolExecutor(max_workers=5) as pool:
         writes = _write_batch_inputs(path, ob_c, ob_k, nt_c, nt_k, pos, ret, pool)
 
-        from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
-
-        for M in f["num_resampled_particles"]:
-            print(M)
-            N = int(M) * (2 * K + K * K)
-            model = two_group.CaseControlModel(
-                mu, sigma, theta, minimum_duration=int(f["minimum_duration"]), omega_case=float(f["omega_case"]),
-                merge_log_prob=float(f["merge_log_prob"]), split_prob=float(f["split_prob"]),
-                num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
-                max_total_reads=max_reads, max_duration=T + 1, multinomial=bool(f["multinomial"]))
-            t0 = time.time()
-            try:
-                res, _final_w, ex = two_group.run({"control": ob_c, "case": ob_k}, {"control": nt_c, "case": nt_k},
-                                                  model, seed, chain_id(chrom, batch))
-            finally:
-                model.close()
-            times[N] = time.time() - t0
-            log_z[N] = float(ex["log_z"])
-            pr = res.particle
-            for name, arr in ((f"optimal_backward_particles_merged_state_{N}_{seed}",
-                               pr["merged_state"].astype(np.int16)[ret]),
-                              (f"optimal_backward_particles_control_state_{N}_{seed}",
-                               pr["control_state"].astype(np.int16)[ret]),
-                              (f"optimal_backward_particles_case_state_{N}_{seed}",
-                               pr["case_state"].astype(np.int16)[ret]),
-                              (f"optimal_split_probs_{N}_{seed}", ex["split_probs"]),
-                              (f"optimal_regime_probs_{N}_{seed}", ex["regime_probs"])):
-                writes.append(pool.submit(np.savez_compressed, os.path.join(path, name), arr))
+        try:
+            _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c, nt_k, max_reads, ret, path,
+                        pool, writes, log_z, times)
+        except BaseException:
+            _report_write_errors(writes)
+            raise
         for w in writes:
             w.result()
     with open(os.path.join(path, f"log_normalizing_constants_optimal_{seed}.txt"), "w") as fh:
@@ -312,6 +290,52 @@ def infer(argv: Sequence[str]) -> int:
     with open(os.path.join(path, f"optimal_time_backward_{seed}.txt"), "w") as fh:
         print({}, file=fh)
     return 0
+
+
+def _report_write_errors(writes) -> None:
+    """On a failed run: wait for the result writes already submitted and report
+    any of them that failed too (the run's own exception is the one raised)."""
+    from concurrent.futures import wait
+
+    done, _ = wait(writes)
+    for w in done:
+        e = w.exception()
+        if e is not None:
+            print(f"hygeia: a result-file write failed as well: {e!r}", file=sys.stderr)
+
+
+def _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c, nt_k, max_reads, ret, path, pool,
+                writes, log_z, times) -> None:
+    """The chain runs of one `hygeia infer` task, one per --num_resampled_particles
+    value (run_inference_two_groups.py:263-322); result writes go to `pool`."""
+    from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
+
+    for M in f["num_resampled_particles"]:
+        print(M)
+        N = int(M) * (2 * K + K * K)
+        model = two_group.CaseControlModel(
+            mu, sigma, theta, minimum_duration=int(f["minimum_duration"]), omega_case=float(f["omega_case"]),
+            merge_log_prob=float(f["merge_log_prob"]), split_prob=float(f["split_prob"]),
+            num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
+            max_total_reads=max_reads, max_duration=T + 1, multinomial=bool(f["multinomial"]))
+        t0 = time.time()
+        try:
+            res, _final_w, ex = two_group.run({"control": ob_c, "case": ob_k}, {"control": nt_c, "case": nt_k},
+                                              model, seed, chain_id(chrom, batch))
+        finally:
+            model.close()
+        times[N] = time.time() - t0
+        log_z[N] = float(ex["log_z"])
+        pr = res.particle
+        for name, arr in ((f"optimal_backward_particles_merged_state_{N}_{seed}",
+                           pr["merged_state"].astype(np.int16)[ret]),
+                          (f"optimal_backward_particles_control_state_{N}_{seed}",
+                           pr["control_state"].astype(np.int16)[ret]),
+                          (f"optimal_backward_particles_case_state_{N}_{seed}",
+                           pr["case_state"].astype(np.int16)[ret]),
+                          (f"optimal_split_probs_{N}_{seed}", ex["split_probs"]),
+                          (f"optimal_regime_probs_{N}_{seed}", ex["regime_probs"])):
+            writes.append(pool.submit(np.savez_compressed, os.path.join(path, name), arr))
 
 
 def _write_batch_inputs(path: str, ob_c, ob_k, nt_c, nt_k, pos, ret, pool=None):

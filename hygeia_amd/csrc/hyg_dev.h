@@ -4,9 +4,26 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../../include/hyg_arith.h"
 
 namespace hyg {
+
+// Tuning and profiling switches read from the environment (HYG_THREADS,
+// HYG_THREADS_FWD / _BWD, HYG_LOWOCC_THREADS, HYG_NO_SHAPE, HYG_TOPSET_R,
+// HYG_DEBUG_PHASES, HYG_SG_PHASES) exist only in a build made with -DHYG_TUNING
+// (`bash tools/build_variant.sh tuning -DHYG_TUNING`, selected with
+// HYG_LIB_PATH). The default library never reads them, so an inherited
+// environment cannot change which kernels it launches.
+inline const char* tuning_env(const char* name) {
+#ifdef HYG_TUNING
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // ----------------------------------------------------------- small helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }

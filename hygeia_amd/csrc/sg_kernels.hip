@@ -1517,7 +1517,7 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
   if (pe) ped = *pe;
   if (lds > kSgLdsBudget) return HYG_EUNSUPPORTED;
   // phase timers: HYG_SG_PHASES=1, in the K = 6 instantiations (the pipeline's shape) only
-  static const bool want_env = getenv("HYG_SG_PHASES") != nullptr;
+  static const bool want_env = tuning_env("HYG_SG_PHASES") != nullptr;
   const bool want_dbg = want_env && c.K == 6;
   unsigned long long* dbg = nullptr;
   hipStream_t s = (hipStream_t)stream;

@@ -2679,23 +2679,23 @@ int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
   static int lowocc = -1;  // 0: the defaults kLowOccThreads / kLowOccThreadsBwd
   const int k = backward ? 1 : 0;
   if (env[k] < 0) {
-    const char* v = getenv(backward ? "HYG_THREADS_BWD" : "HYG_THREADS_FWD");
-    if (!v) v = getenv("HYG_THREADS");
+    const char* v = tuning_env(backward ? "HYG_THREADS_BWD" : "HYG_THREADS_FWD");
+    if (!v) v = tuning_env("HYG_THREADS");
     const int x = v ? atoi(v) : 0;
     env[k] = valid_width(x) ? x : 0;
   }
   if (lowocc < 0) {
-    const char* v = getenv("HYG_LOWOCC_THREADS");
+    const char* v = tuning_env("HYG_LOWOCC_THREADS");
     const int x = v ? atoi(v) : 0;
     lowocc = (x == 256 || x == 512 || x == 768) ? x : 0;
   }
   if (env[k]) return env[k];
   const int def = backward ? kDefaultThreadsBwd : kDefaultThreads;
+  if (c.M > 64) return def;  // the wider kernels assume the pipeline's M <= 64 (one ancestor per lane)
   const size_t lds = make_layout(c.K, c.M, c.B, c.Nmax, def, false).total;
   // (C5: the backward's list path keeps its 12 waves busy: 768 threads, 6 %
   // faster than 512 in r03d; the forward is faster at 512)
   if (2 * lds > 160 * 1024) return backward ? 768 : 512;
-  if (c.M > 64) return def;  // the wider kernels assume the pipeline's M <= 64 (one ancestor per lane)
   if (n_chains <= device_cus()) return lowocc ? lowocc : (backward ? kLowOccThreadsBwd : kLowOccThreads);
   return def;
 }
@@ -2750,17 +2750,17 @@ int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* 
 using FwdFn = decltype(&tg_forward_kernel<64>);
 using BwdFn = decltype(&tg_backward_kernel<64>);
 static bool shape_specialised(const hyg_tg_consts& c) {
-  static const bool off = getenv("HYG_NO_SHAPE") != nullptr;
+  static const bool off = tuning_env("HYG_NO_SHAPE") != nullptr;
   return !off && c.K == 6 && c.M == 50 && c.B == 25 && c.I == 48 && c.Nmax == 2400;
 }
 // the stress shape (C5: K = 12, M = 50, B = 25), one chain per CU at 512 threads
 static bool shape_c5(const hyg_tg_consts& c) {
-  static const bool off = getenv("HYG_NO_SHAPE") != nullptr;
+  static const bool off = tuning_env("HYG_NO_SHAPE") != nullptr;
   return !off && c.K == 12 && c.M == 50 && c.B == 25 && c.I == 168 && c.Nmax == 8400;
 }
 // HYG_DEBUG_PHASES=1 selects the phase-timer instantiations (256 and 512 threads).
 static bool want_phases() {
-  static const bool on = getenv("HYG_DEBUG_PHASES") != nullptr;
+  static const bool on = tuning_env("HYG_DEBUG_PHASES") != nullptr;
   return on;
 }
 template <int NT>
@@ -2799,7 +2799,7 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
                             const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
   Lay lf = make_layout(c.K, c.M, c.B, c.Nmax, NT, false);
   if (lf.total > 160 * 1024) return HYG_EUNSUPPORTED;
-  static const char* rv = getenv("HYG_TOPSET_R");  // tuning: 1 (A <= 64 per wave) or 2
+  static const char* rv = tuning_env("HYG_TOPSET_R");  // tuning: 1 (A <= 64 per wave) or 2
   if (rv && (atoi(rv) == 1 || atoi(rv) == 2)) lf.topset_r = atoi(rv);
   if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
   if (hipFuncSetAttribute((const void*)fwd_kernel<NT>(c), hipFuncAttributeMaxDynamicSharedMemorySize,

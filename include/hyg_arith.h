@@ -293,9 +293,11 @@ HYG_HD hyg_u128 hyg_fix100(double e) {
  * (0.7, 1.42), scaled by a power of two without rounding), so
  * floor(e 2^100) = m 2^(E_p + k + 48) for p's 53-bit significand m and exponent
  * E_p -- a shift, no float floors. Below -70 the exact image is 0
- * (e^x 2^100 < 1 for x < -69.32); x >= 11 (e >= 65536 is 0 in hyg_fix100) does
- * not occur on the paths that use it (x <= 0) and is also mapped to 0.
- * tests/test_arith.py checks the two forms integer for integer. */
+ * (e^x 2^100 < 1 for x < -69.32). The identity is claimed for x <= 0 only,
+ * the only range its callers pass (x - max of a set): for x >= 11 this returns
+ * 0 while hyg_fix100(hyg_exp(x)) stays nonzero up to ln 65536 = 11.09, so a
+ * caller with x > 0 must use hyg_fix100(hyg_exp(x)).
+ * tests/test_arith.py checks the two forms integer for integer on x <= 0. */
 HYG_HD hyg_u128 hyg_exp_fix100_pk(double p, int k, double x) {
   const uint64_t pb = hyg_f64_bits(p);
   const int sh = (int)((pb >> 52) & 0x7ff) - 1023 + k + 48; /* in [-54, 64] on the range */

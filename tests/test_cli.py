@@ -175,3 +175,37 @@ def test_read_matrix_equals_pandas(tmp_path):
         ref = pd.read_csv(p, sep=",", header=None, dtype=np.float64).to_numpy()
         assert got.dtype == np.float64 and got.shape == ref.shape
         assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), name
+
+
+@pytest.mark.parametrize("group", ["case", "control"])
+@pytest.mark.parametrize("cmd", ["infer", "infer_many"])
+def test_methylated_above_total_is_rejected(tmp_path, group, cmd):
+    """A site whose methylated count exceeds its total count stops the task with
+    an AssertionError before any chain runs, in either group.
+
+    The reference asserts this for the case group only: its control assertion
+    compares n_total_reads_control with itself (run_inference_two_groups.py:
+    210-211) and can never fail. That input has no defined emission
+    (Beta-Binomial with k > n: TFP returns -inf or NaN from its lgamma terms),
+    so the build applies the check the assertion evidently means to both groups
+    -- a deliberate divergence at the boundary."""
+    _write_inputs(str(tmp_path), "21", 300)
+    f = tmp_path / "data" / f"n_methylated_reads_{group}_21.txt.gz"
+    tot = np.loadtxt(tmp_path / "data" / f"n_total_reads_{group}_21.txt.gz", delimiter=",")
+    meth = np.loadtxt(f, delimiter=",")
+    meth[150, 1] = tot[150, 1] + 1  # inside batch 1's rows [90, 210)
+    np.savetxt(f, meth, fmt="%s", delimiter=",")
+    args = [cmd, "--chrom", "21", "--segment_size", "100", "--buffer_size", "10",
+            "--data_dir", str(tmp_path / "data"), "--single_group_dir", str(tmp_path / "sg"),
+            "--results_dir", str(tmp_path / "res")]
+    args += ["--batch", "1"] if cmd == "infer" else ["--batches", "1"]
+    with pytest.raises(AssertionError, match="methylated reads exceed total reads"):
+        cli.main(args)
+    # a batch whose rows do not hold the site runs on (up to the device call)
+    args_ok = [a if a != "1" else "2" for a in args]
+    try:
+        cli.main(args_ok)  # runs on a GPU host; stops at the device call without one
+    except AssertionError:
+        raise
+    except Exception:
+        pass

@@ -8,7 +8,9 @@ Each configuration runs many seeds as chains of ONE batched launch
     given the phantom regime to 1e-12 and the GPU's backward draws pass the
     chi-square tests against the exact smoother; with M = 2-3 (optimal
     finite-state resampling active) the seed average of Z_hat / Z stays 1
-    within its standard error. Cases at u = 2, the pipeline's u = 3, and u = 4.
+    within its standard error. Cases at u = 2, the pipeline's u = 3, and u = 4,
+    and (round 4) at the pipeline's K = 6 and K = 4 with 2 + 2 samples, where
+    the case transition's uniform normalisers are 1/5 and 1/4.
 """
 import math
 import os
@@ -121,3 +123,72 @@ def test_backward_gpu_draws_follow_exact_smoother(oracle, K, T, dseed, u):
         return mg[i * T:(i + 1) * T], ct[i * T:(i + 1) * T], cs[i * T:(i + 1) * T]
 
     check_draws_follow_exact_smoother(oracle, ex, E_ex, K, T, u, B, seeds, cid, paths_of)
+
+
+# ----------------------------------------------------- the pipeline's K (4, 6)
+from test_tg_exact import (PIPELINE_BACKWARD, PIPELINE_KEEP_ALL, PIPELINE_RESAMPLING,  # noqa: E402
+                           draws_branch_counts)
+
+
+@pytest.mark.parametrize("K,T,dseed,u,S,M", [c[:6] for c in PIPELINE_KEEP_ALL if c[6]])
+def test_pipeline_k_keep_all_gpu_vs_oracle_and_exact(oracle, K, T, dseed, u, S, M):
+    """K = 6 / K = 4, u = 3, 2 + 2 samples, every finite particle kept: the GPU's
+    log Z is the exact log marginal likelihood (1e-12), bit for bit the oracle."""
+    B = 8
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=B, u=u, S=S)
+    seeds = list(range(24))
+    cid = 40
+    dc = _run_seeds(p, E, K, M, B, seeds, cid)
+    lz = dc.log_z.cpu().numpy()
+    exact = {}
+    for i, s in enumerate(seeds):
+        _check_chain_bits(oracle, p, E, dc, i, s, cid, T)
+        r_ph = phantom_regime(oracle, s, cid, K)
+        if r_ph not in exact:
+            exact[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+        assert abs(lz[i] - exact[r_ph]) < 1e-12 * max(1.0, abs(exact[r_ph]))
+    assert len(exact) >= 2
+
+
+@pytest.mark.parametrize("K,T,M,dseed,u,S", PIPELINE_RESAMPLING)
+def test_pipeline_k_resampling_gpu_unbiased_z(oracle, K, T, M, dseed, u, S):
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2, u=u, S=S)
+    seeds = list(range(8192))
+    cid = 3
+    dc = _run_seeds(p, E, K, M, 2, seeds, cid)
+    for i in range(0, len(seeds), 511):
+        _check_chain_bits(oracle, p, E, dc, i, seeds[i], cid, T)
+    lz = dc.log_z.cpu().numpy()
+    zex = {}
+    ratios = []
+    for i, s in enumerate(seeds):
+        r_ph = phantom_regime(oracle, s, cid, K)
+        if r_ph not in zex:
+            zex[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+        ratios.append(math.exp(lz[i] - zex[r_ph]))
+    r = np.array(ratios)
+    se = r.std() / math.sqrt(len(r))
+    assert abs(r.mean() - 1.0) < 4 * se + 1e-3, (r.mean(), se)
+    assert r.std() > 1e-3
+
+
+@pytest.mark.parametrize("K,T,dseed,u,S,M", [c[:6] for c in PIPELINE_BACKWARD if c[6]])
+def test_pipeline_k_backward_gpu_draws_follow_exact_smoother(oracle, K, T, dseed, u, S, M):
+    B, nseeds, cid = 60, 300, 7
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=B, cov=2, u=u, S=S)
+    seeds = list(range(nseeds))
+    dc = _run_seeds(p, E, K, M, B, seeds, cid)
+    for i in range(0, nseeds, 37):
+        _check_chain_bits(oracle, p, E, dc, i, seeds[i], cid, T)
+    mg, ct, cs = dc.merged.cpu().numpy(), dc.control.cpu().numpy(), dc.case.cpu().numpy()
+
+    def paths_of(i, seed):
+        return mg[i * T:(i + 1) * T], ct[i * T:(i + 1) * T], cs[i * T:(i + 1) * T]
+
+    check_draws_follow_exact_smoother(oracle, ex, E_ex, K, T, u, B, seeds, cid, paths_of)
+    paths = []
+    for i in range(nseeds):
+        m, c, k = (a.astype(int) for a in paths_of(i, seeds[i]))
+        paths += [[(m[t, b], c[t, b, 0], c[t, b, 1], k[t, b, 0], k[t, b, 1]) for t in range(T)] for b in range(B)]
+    n = draws_branch_counts(ex, paths)
+    assert n[(2, True)] > 0 and n[(4, True)] > 0, dict(n)

@@ -44,7 +44,7 @@ RESAMPLING_CASES = [(3, 8, 3, 24, 2), (3, 5, 3, 22, 2), (2, 7, 2, 23, 2), (3, 8,
                     (3, 8, 3, 27, 4)]
 
 
-def _problem(oracle, K, T, seed, M, B, cov=12, p_random=True, u=2):
+def _problem(oracle, K, T, seed, M, B, cov=12, p_random=True, u=2, S=1):
     rng = np.random.default_rng(seed)
     mu = [(i + 0.5) / K for i in range(K)]
     sg = [0.08 + 0.04 * (i % 2) for i in range(K)]
@@ -59,12 +59,13 @@ def _problem(oracle, K, T, seed, M, B, cov=12, p_random=True, u=2):
         theta = None
     p = oracle.make_params(K=K, M=M, B=B, mu=mu, sigma=sg, theta=theta, u=u)
     theta = np.array(p.theta[: p.theta_len])
-    tot = rng.poisson(cov, size=(T, 2)).astype(np.uint16)
+    tot = rng.poisson(cov, size=(T, 2 * S)).astype(np.uint16)
     # methylation levels drawn from the regimes, with a change in the case group
-    lev = np.where(np.arange(T)[:, None] < T // 2, 0.2, 0.8) * np.array([[1.0, 0.5]]) + np.array([[0.1, 0.3]])
+    lev = np.where(np.arange(T)[:, None] < T // 2, 0.2, 0.8) * np.repeat(np.array([[1.0, 0.5]]), S, 1) + \
+        np.repeat(np.array([[0.1, 0.3]]), S, 1)
     meth = rng.binomial(tot.astype(np.int64), np.clip(lev, 0.01, 0.99)).astype(np.uint16)
-    d = {"meth_control": meth[:, :1].copy(), "tot_control": tot[:, :1].copy(),
-         "meth_case": meth[:, 1:].copy(), "tot_case": tot[:, 1:].copy()}
+    d = {"meth_control": meth[:, :S].copy(), "tot_control": tot[:, :S].copy(),
+         "meth_case": meth[:, S:].copy(), "tot_case": tot[:, S:].copy()}
     ex = ExactModel(K, mu, sg, theta, u=u)
     E = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
     E_ex = ex.emission(d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
@@ -203,4 +204,144 @@ def test_resampling_keeps_z_unbiased(oracle, K, T, M, dseed, u):
     se = r.std() / math.sqrt(len(r))
     assert abs(r.mean() - 1.0) < 4 * se + 1e-3, (r.mean(), se, dict(modes))
     # the estimate is not degenerate: resampling actually adds variance
+    assert r.std() > 1e-3
+
+
+# ---------------------------------------------------------------------------
+# The pipeline's K. K = 6 is the shape every BASELINE configuration but C5 runs
+# (K = 12); K = 4 sits between. These are the first shapes at which the three
+# uniform regime draws of the case transition (case_control_distributions.py:
+# 246-291) have normalisers other than 1 and 1/2: branch 2 (a merged ancestor
+# splits, the control continues) draws r_k' over K - 1 regimes, branch 3 over
+# K - 1, branch 4 (the case changes while the control changed or moved
+# elsewhere) over K - 2 -- at K = 6: 1/5, 1/5 and 1/4. u = 3 (the pipeline's
+# min_cpg_sites_between_change_points) and 2 + 2 samples.
+#
+# Keep-all regime: at step t the filter keeps every finite particle of step
+# t - 1, so M must cover the finite count of step T - 2: K = 6 has 5, 5, 5,
+# 180, 680 paths at t = 0..4; K = 4 has 3, 3, 3, 48, 156. The GPU holds
+# M <= 165 at K = 6 in LDS (N = 48 M candidates), so K = 6, T = 5 (M = 192)
+# is a CPU (oracle) case only; the GPU runs K = 6 up to T = 4 and K = 4 up to
+# T = 6 in the keep-all regime, and K = 6, T = 7 with resampling.
+# (K, T, data seed, u, samples per group, M, gpu)
+PIPELINE_KEEP_ALL = [(6, 4, 71, 3, 2, 64, True), (4, 5, 72, 3, 2, 64, True), (4, 6, 73, 3, 2, 160, True),
+                     (6, 5, 74, 3, 2, 192, False)]
+PIPELINE_BACKWARD = [(6, 4, 81, 3, 2, 64, True), (4, 5, 82, 3, 2, 64, True), (6, 5, 83, 3, 2, 192, False)]
+# (K, T, M, data seed, u, samples per group): optimal finite-state resampling active
+PIPELINE_RESAMPLING = [(6, 7, 4, 91, 3, 2), (6, 6, 10, 92, 3, 2), (4, 8, 6, 93, 3, 2)]
+
+
+def branch_mass(ex, pair):
+    """Posterior mass of the case transition's branches over the sites of a
+    chain, from the exact pairwise smoothing marginals: {(branch, change):
+    expected number of such transitions}, change = the case regime is redrawn
+    (d_k' = 1 outside branch 1)."""
+    out = Counter()
+    for d in pair:
+        for (x, y), pr in d.items():
+            b = ex.case_branch(x, y)
+            out[(b, b != 1 and y[3] == 1)] += pr
+    return out
+
+
+def test_pipeline_k_visits_every_case_branch(oracle):
+    """The K = 6 cases exercise the case transition's K-dependent normalisers:
+    the exact smoother puts mass on branch 2 (1/(K-1) = 1/5), branch 3 (1/5) and
+    a branch-4 change (1/(K-2) = 1/4), and replacing any of those normalisers by
+    its neighbour moves the exact log Z by far more than the 1e-12 the keep-all
+    tests allow -- so those tests pin them."""
+    for K, T, dseed, u, S, M, _ in [c for c in PIPELINE_KEEP_ALL if c[0] == 6]:
+        p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=4, u=u, S=S)
+        r_ph = phantom_regime(oracle, 0, 40, K)
+        log_z, _, _, pair = ex.forward_backward(E_ex, r_ph)
+        mass = branch_mass(ex, pair)
+        assert mass[(2, True)] > 1e-6, dict(mass)
+        assert mass[(4, True)] > 1e-6, dict(mass)
+        if T >= 5:  # a split ancestor whose control moves onto the case regime needs t >= u + 1
+            assert mass[(3, True)] > 1e-9, dict(mass)
+        for branch, size in ((2, K - 2), (4, K - 1)) + (((3, K - 2),) if T >= 5 else ()):
+            wrong = ExactModel(K, [p.mu[i] for i in range(K)], [p.sigma[i] for i in range(K)],
+                               np.array(p.theta[: p.theta_len]), u=u, case_uniform_sizes={branch: size})
+            lz_wrong = wrong.forward_backward(E_ex, r_ph)[0]
+            # at least 100 x the keep-all tolerance (1e-12 relative)
+            assert abs(lz_wrong - log_z) > 1e-10 * abs(log_z), (branch, lz_wrong, log_z)
+
+
+@pytest.mark.parametrize("K,T,dseed,u,S,M,gpu", PIPELINE_KEEP_ALL)
+def test_pipeline_k_keep_all_log_z_and_filter_marginal(oracle, K, T, dseed, u, S, M, gpu):
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=4, u=u, S=S)
+    seen = set()
+    for seed in range(8):
+        cid = 40 + seed
+        out = oracle.chain(p, E, seed, cid, want_modes=True)
+        assert out["status"] == 0
+        assert np.all(out["modes"][1:] // 65536 == MODE_KEEP), "M too small for the keep-all regime"
+        r_ph = phantom_regime(oracle, seed, cid, K)
+        seen.add(r_ph)
+        log_z, alphas, _, _ = ex.forward_backward(E_ex, r_ph)
+        assert abs(out["log_z"] - log_z) < 1e-12 * max(1.0, abs(log_z)), (out["log_z"], log_z)
+        w, st = out["final_log_weights"], out["final_states"]
+        fin = np.isfinite(w)
+        pooled = Counter()
+        for s, lw in zip(st[fin], w[fin]):
+            pooled[unpack(s)] += math.exp(lw - out["log_z"])
+        exact = {x: math.exp(a - log_z) for x, a in alphas[-1].items()}
+        assert set(pooled) == set(exact)
+        for x in exact:
+            assert abs(pooled[x] - exact[x]) < 1e-12, (x, pooled[x], exact[x])
+    assert len(seen) >= 2
+
+
+def draws_branch_counts(ex, paths):
+    """Case-branch transitions in drawn trajectories: {(branch, change): n}."""
+    out = Counter()
+    for path in paths:
+        for x, y in zip(path[:-1], path[1:]):
+            b = ex.case_branch(x, y)
+            out[(b, b != 1 and y[3] == 1)] += 1
+    return out
+
+
+@pytest.mark.parametrize("K,T,dseed,u,S,M,gpu", PIPELINE_BACKWARD)
+def test_pipeline_k_backward_draws_follow_exact_smoother(oracle, K, T, dseed, u, S, M, gpu):
+    B, nseeds = 60, 300
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=B, cov=2, u=u, S=S)
+    outs = {}
+
+    def paths_of(i, seed):
+        out = oracle.chain(p, E, seed, 7)
+        assert out["status"] == 0
+        outs[seed] = out
+        return out["merged"], out["control"], out["case"]
+
+    check_draws_follow_exact_smoother(oracle, ex, E_ex, K, T, u, B, range(nseeds), 7, paths_of)
+    # the draws themselves take the K-dependent branches
+    paths = []
+    for out in outs.values():
+        m, c, k = (a.astype(int) for a in (out["merged"], out["control"], out["case"]))
+        paths += [[(m[t, b], c[t, b, 0], c[t, b, 1], k[t, b, 0], k[t, b, 1]) for t in range(T)] for b in range(B)]
+    n = draws_branch_counts(ex, paths)
+    assert n[(2, True)] > 0 and n[(4, True)] > 0, dict(n)
+
+
+@pytest.mark.parametrize("K,T,M,dseed,u,S", PIPELINE_RESAMPLING)
+def test_pipeline_k_resampling_keeps_z_unbiased(oracle, K, T, M, dseed, u, S):
+    nseeds = 12000
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2, u=u, S=S)
+    zex = {}
+    ratios = []
+    modes = Counter()
+    for seed in range(nseeds):
+        cid = 3
+        r_ph = phantom_regime(oracle, seed, cid, K)
+        if r_ph not in zex:
+            zex[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+        out = oracle.chain(p, E, seed, cid, want_modes=True)
+        assert out["status"] == 0
+        modes.update((out["modes"][1:] // 65536).tolist())
+        ratios.append(math.exp(out["log_z"] - zex[r_ph]))
+    assert modes[MODE_OPTIMAL] > nseeds
+    r = np.array(ratios)
+    se = r.std() / math.sqrt(len(r))
+    assert abs(r.mean() - 1.0) < 4 * se + 1e-3, (r.mean(), se, dict(modes))
     assert r.std() > 1e-3

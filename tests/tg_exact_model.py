@@ -43,8 +43,12 @@ f32 = lambda x: float(np.float32(x))  # noqa: E731
 
 class ExactModel:
     def __init__(self, K, mu, sigma, theta, u=3, omega_case=0.8, merge_log_prob=math.log(0.1), split_prob=0.01,
-                 kappa=2.0):
+                 kappa=2.0, case_uniform_sizes=None):
         self.K, self.u = K, u
+        # sizes of the case transition's uniform regime draws per branch (2, 3, 4);
+        # None = the reference's allowed sets. Tests override one of them to show
+        # that the log Z comparison would catch a wrong normaliser.
+        self.case_uniform_sizes = case_uniform_sizes or {}
         mu = np.array([f32(v) for v in mu])
         sg = np.array([f32(v) for v in sigma])
         nu = mu * (1 - mu) / sg ** 2 - 1
@@ -114,22 +118,43 @@ class ExactModel:
         else:
             lc = _log(1 - rho_c) if (dc2 == dc + 1 and rc2 == rc) else -np.inf
         # case (case_control_distributions.py:246-291)
-        if m2 == 1:
+        branch = self.case_branch(x, y)
+        sz = lambda allowed: self.case_uniform_sizes.get(branch, len(allowed))  # noqa: E731
+        if branch == 1:
             lk = 0.0 if (rk2 == rc2 and dk2 == dc2) else -np.inf
-        elif m == 1 and dc2 != 1:
+        elif branch == 2:
             allowed = [r for r in range(K) if r != rc2]
-            lk = -math.log(len(allowed)) if (dk2 == 1 and rk2 in allowed) else -np.inf
-        elif rc2 == rk and m == 0:
+            lk = -math.log(sz(allowed)) if (dk2 == 1 and rk2 in allowed) else -np.inf
+        elif branch == 3:
             allowed = [r for r in range(K) if r != rc2 and r != rk]
-            lk = -math.log(len(allowed)) if (dk2 == 1 and rk2 in allowed and allowed) else -np.inf
+            lk = -math.log(sz(allowed)) if (dk2 == 1 and rk2 in allowed and allowed) else -np.inf
         else:
             rho_k = self.rho(1, rk, dk)
             if dk2 == 1:
                 allowed = [r for r in range(K) if r != rc2 and r != rk]
-                lk = _log(rho_k) - math.log(len(allowed)) if (rk2 in allowed) else -np.inf
+                lk = _log(rho_k) - math.log(sz(allowed)) if (rk2 in allowed) else -np.inf
             else:
                 lk = _log(1 - rho_k) if (dk2 == dk + 1 and rk2 == rk) else -np.inf
         return lm + lc + lk
+
+    @staticmethod
+    def case_branch(x, y):
+        """Which of the four branches of CaseStateTransition._log_prob
+        (case_control_distributions.py:246-291) scores the case part of x -> y:
+        1 merged next state; 2 a merged ancestor splits while the control
+        continues (case regime uniform over r != r_c', 1/(K-1)); 3 a split
+        ancestor whose control moves onto the case regime (uniform over
+        r not in {r_c', r_k}, here 1/(K-1)); 4 otherwise (hazard rho_k, a change
+        uniform over r not in {r_c', r_k}: 1/(K-2) when r_c' != r_k)."""
+        m, _, _, _, rk = x
+        m2, dc2, rc2, _, _ = y
+        if m2 == 1:
+            return 1
+        if m == 1 and dc2 != 1:
+            return 2
+        if rc2 == rk and m == 0:
+            return 3
+        return 4
 
     def successors(self, x):
         m, dc, rc, dk, rk = x

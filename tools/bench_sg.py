@@ -91,10 +91,11 @@ def cpu_baseline(meth, tot, chains, params, seconds, threads, pe=False, refstruc
     for t in th:
         t.join()
     dt = time.perf_counter() - t0
-    what = ("oracle_sg_chain_refstruct (the reference's structure: Beta-Binomial from the counts at every use) "
+    what = ("oracle_sg_chain_refstruct (the reference's emission structure: Beta-Binomial from the counts at "
+            "every use; the backward-kernel rows factorised as in the port, not the reference's per-row exps) "
             if refstruct else "oracle/sg_oracle.c emission + ")
     return {"value": sum(res) / dt, "unit": "CpG-sites/s", "cores": threads, "kind": "port",
-            "variant": "reference structure" if refstruct else "optimised port",
+            "variant": "reference emission structure, factorised backward kernels" if refstruct else "optimised port",
             "sample": f"{threads} threads x {n}-site prefixes of the chromosome chains, each one "
                       f"{what}SMC + online smoothing"
                       f"{' + online parameter estimation' if pe else ''}; {sum(res)} sites in {dt:.1f} s"}
@@ -235,7 +236,7 @@ def main():
                   + (" + online parameter estimation" if pe is not None else ""), "value": units / (ms / 1000.0),
         "unit": "CpG-site-samples/s" if args.per_sample else "CpG-sites/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": (f"C2 single_group {args.sites} CpG x {args.samples} samples, one chain per "
                                 f"(sample, chromosome) = {len(chains)} chains of 1 sample" if args.per_sample else
                                 f"C1 single_group chr21 {args.sites} CpG, one chain, {S} samples" if c1 else
