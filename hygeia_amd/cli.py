@@ -143,6 +143,13 @@ def serialize_flags(f: Dict[str, object]) -> str:
     return "\n".join(lines)
 
 
+# Wall-clock phase split of the last infer / infer_many call in this process
+# (seconds): parse (the chromosome's input files), device (model, chains, copies
+# back), writes (joining the result-file writes after the last chain). Read by
+# tools/bench_pipeline.py; nothing in the command's behaviour depends on it.
+LAST_TIMINGS: Dict[str, float] = {}
+
+
 def chain_id(chrom: str, batch: int) -> int:
     return (zlib.crc32(str(chrom).encode()) << 32) | (int(batch) & 0xFFFFFFFF)
 
@@ -248,7 +255,10 @@ def infer(argv: Sequence[str]) -> int:
     if theta.shape[0] != K * K:
         raise ValueError(f"theta_{chrom}.csv.gz holds {theta.shape[0]} values, expected K^2 = {K * K}")
 
+    LAST_TIMINGS.clear()
+    t_parse = time.perf_counter()
     positions, tot_c, meth_c, tot_k, meth_k = _read_inputs(str(f["data_dir"]), chrom)
+    LAST_TIMINGS["parse"] = time.perf_counter() - t_parse
 
     seg = segment_index(positions.shape[0], batch, int(f["segment_size"]), int(f["buffer_size"]))
     if seg is None:
@@ -275,14 +285,18 @@ def infer(argv: Sequence[str]) -> int:
     with ThreadPoolExecutor(max_workers=5) as pool:
         writes = _write_batch_inputs(path, ob_c, ob_k, nt_c, nt_k, pos, ret, pool)
 
+        t_dev = time.perf_counter()
         try:
             _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c, nt_k, max_reads, ret, path,
                         pool, writes, log_z, times)
         except BaseException:
             _report_write_errors(writes)
             raise
+        t_w = time.perf_counter()
+        LAST_TIMINGS["device"] = t_w - t_dev
         for w in writes:
             w.result()
+        LAST_TIMINGS["writes"] = time.perf_counter() - t_w
     with open(os.path.join(path, f"log_normalizing_constants_optimal_{seed}.txt"), "w") as fh:
         print(log_z, file=fh)
     with open(os.path.join(path, f"optimal_time_{seed}.txt"), "w") as fh:
@@ -378,8 +392,11 @@ def infer_many(argv: Sequence[str]) -> int:
     theta = read_theta(str(f["single_group_dir"]), chrom)
     if theta.shape[0] != K * K:
         raise ValueError(f"theta_{chrom}.csv.gz holds {theta.shape[0]} values, expected K^2 = {K * K}")
+    LAST_TIMINGS.clear()
+    t_parse = time.perf_counter()
     positions, tot_c, meth_c, tot_k, meth_k = _read_inputs(str(f["data_dir"]), chrom)
     tot_c, meth_c, tot_k, meth_k = (a.astype(np.float32) for a in (tot_c, meth_c, tot_k, meth_k))
+    LAST_TIMINGS["parse"] = time.perf_counter() - t_parse
     n = positions.shape[0]
     batches = (list(range(0, n // S + 1)) if str(f["batches"]) == "all"
                else [int(x) for x in str(f["batches"]).split(",") if x != ""])
@@ -409,13 +426,17 @@ def infer_many(argv: Sequence[str]) -> int:
         writes.append(pool.submit(_write_batch_inputs, path, meth_c[lo:hi], meth_k[lo:hi], tot_c[lo:hi],
                                   tot_k[lo:hi], positions[lo:hi].astype(np.int64), slice(r0, r1)))
 
+    t_dev = time.perf_counter()
     try:
         return _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, meth_k, tot_k, pool,
                                writes)
     finally:
+        t_w = time.perf_counter()
+        LAST_TIMINGS["device"] = t_w - t_dev  # (includes submitting the result writes)
         for w in writes:  # zlib releases the GIL: the files compress in parallel
             w.result()
         pool.shutdown()
+        LAST_TIMINGS["writes"] = time.perf_counter() - t_w
 
 
 def _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, meth_k, tot_k, pool, writes) -> int:

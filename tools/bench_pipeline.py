@@ -23,6 +23,7 @@ import gzip
 import json
 import os
 import shutil
+import subprocess
 import sys
 import tempfile
 import time
@@ -80,16 +81,35 @@ def main():
                      os.path.join(wd, "many")] + common) == 0
     t_many = time.perf_counter() - t0
     print(f"infer_many done in {t_many:.1f} s", flush=True)
-    t0 = time.perf_counter()
-    assert cli.main(["infer", "--batch", "0", "--seed", str(seeds[0]), "--results_dir", os.path.join(wd, "one")]
-                    + common) == 0
-    t_one = time.perf_counter() - t0
+    many_split = dict(cli.LAST_TIMINGS)
+    # The unchanged Nextflow module runs one `hygeia infer` PROCESS per (batch,
+    # seed) (modules/two_group/4_infer.nf:42-48): each task below is a fresh
+    # Python process (interpreter start, imports, HIP initialisation included),
+    # timed from outside, with the command's own phase split printed by it.
+    drv = ("import json, sys, time; t0 = time.perf_counter(); from hygeia_amd import cli; t1 = time.perf_counter(); "
+           "rc = cli.main(sys.argv[1:]); t2 = time.perf_counter(); "
+           "print('@@' + json.dumps(dict(cli.LAST_TIMINGS, import_cli=t1 - t0, main=t2 - t1, rc=rc)), flush=True)")
+    one = []
+    for b, sd in ((0, seeds[0]), (n_batches // 2, seeds[-1])):
+        t0 = time.perf_counter()
+        r = subprocess.run([sys.executable, "-c", drv, "infer", "--batch", str(b), "--seed", str(sd), "--results_dir",
+                            os.path.join(wd, "one")] + common, cwd=ROOT, capture_output=True, text=True,
+                           env=dict(os.environ, PYTHONPATH=ROOT))
+        wall = time.perf_counter() - t0
+        if r.returncode != 0:
+            raise RuntimeError(f"hygeia infer --batch {b} failed: {r.stderr[-2000:]}")
+        split = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("@@")][-1][2:])
+        one.append({"batch": b, "seed": sd, "process_wall_s": wall,
+                    "split_s": {k: split[k] for k in ("import_cli", "parse", "device", "writes", "main") if k in split}})
+        print(f"task batch {b} seed {sd}: {wall:.1f} s {one[-1]['split_s']}", flush=True)
+    t_one = sum(o["process_wall_s"] for o in one) / len(one)
     tasks = n_batches * len(seeds)
     line = {"metric": "pipeline CpG sites x seeds / s (hygeia infer, gz CSV in -> result files out)",
             "sites": a.sites, "seeds": seeds, "tasks": tasks,
-            "infer_many": {"value": units / t_many, "wall_s": t_many},
+            "infer_many": {"value": units / t_many, "wall_s": t_many, "split_s": many_split},
             "infer_task_by_task": {"value": units / (t_one * tasks), "wall_s_one_task": t_one,
-                                   "extrapolated_s": t_one * tasks},
+                                   "extrapolated_s": t_one * tasks, "tasks_timed": one,
+                                   "note": "each task a fresh process, as the Nextflow module runs it"},
             "input_write_s": t_write}
     print(json.dumps(line), flush=True)
     if a.workdir is None:
