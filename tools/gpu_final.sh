@@ -1,0 +1,46 @@
+# The round's final measurement set on one GPU call, every step under its own
+# time limit, stopping at the first crash / time-out (exit status other than 0):
+#   parity tests; the default bench line (C3, CPU baselines); C4 and C5 on one
+#   GPU; the C3 / C4 shares of 8 ranks (projections) and the C3 share's phase
+#   split (tuning build); single group C2 and C1; the pipeline-level bench; the
+#   rocprofv3 profile set of the default workload (tools/gpu_profile.sh).
+# Outputs: gpurun_out/<tag>/* (only gpurun_out/ comes back from the box; copy
+# gpurun_out/<tag>/out/* and gpurun_out/prof_<tag>/* into profiles/ afterwards).
+# usage: bash tools/gpu_final.sh <tag>
+set -u
+export TMPDIR=/tmp
+tag=$1
+O=gpurun_out/$tag
+mkdir -p $O
+TUNE=hygeia_amd/lib/var_tuning/libhygeia_amd.so
+( nproc; python3 -c 'import os; print(len(os.sched_getaffinity(0)), os.environ.get("OMP_NUM_THREADS"))'; cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo ) > $O/host.txt 2>&1
+step() {  # step <name> <seconds> <command...>
+  local name=$1 secs=$2; shift 2
+  echo "[$name] $*"
+  timeout -k 10 $secs "$@" > $O/$name.log 2>&1
+  local rc=$?
+  grep '^{' $O/$name.log | tail -1 | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "[$name] rc=$rc: stop"; tail -20 $O/$name.log; exit $rc; fi
+}
+step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+tail -2 $O/tests.log
+step bench_c3 600 python bench.py
+step bench_c4 600 python bench.py --job c4 --steps 1 --warmup 1 --no-cpu-baseline
+step bench_c5 600 python bench.py --job c5 --steps 1 --warmup 1 --no-cpu-baseline
+step bench_c3_shard0of8 300 python bench.py --shard 0/8 --no-cpu-baseline --steps 2
+step bench_c4_shard0of8 300 python bench.py --job c4 --shard 0/8 --no-cpu-baseline --steps 1
+if [ -f $TUNE ]; then
+  step phases_c3_shard0of8 300 env HYG_LIB_PATH=$TUNE HYG_DEBUG_PHASES=1 python bench.py --shard 0/8 --no-cpu-baseline --steps 1 --warmup 0
+fi
+step bench_c2 600 python tools/bench_sg.py
+step bench_c1 600 python tools/bench_sg.py --config c1
+step bench_pipe 600 python tools/bench_pipeline.py
+bash tools/gpu_profile.sh $tag > $O/profile.log 2>&1; rc=$?
+tail -5 $O/profile.log
+mkdir -p $O/out
+for n in bench_c3 bench_c4 bench_c5 bench_c3_shard0of8 bench_c4_shard0of8 bench_c2 bench_c1 bench_pipe; do
+  grep '^{' $O/$n.log | tail -1 > $O/out/${tag}_$n.json
+done
+grep -h "phases" $O/phases_c3_shard0of8.log > $O/out/${tag}_phases_c3_shard0of8.log 2>/dev/null
+cp $O/host.txt $O/out/${tag}_host.txt
+exit $rc
