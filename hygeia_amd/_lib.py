@@ -131,19 +131,37 @@ class DmpGroup(C.Structure):
 _lib = None
 
 
-def load() -> C.CDLL:
-    """Loads (building first if needed) the HIP library; raises if impossible."""
-    global _lib
+_with_torch = False  # whether torch was imported before the library loaded
+
+
+def loaded_with_torch() -> bool:
+    """True when the library was loaded after torch (its HIP runtime first)."""
+    return _lib is not None and _with_torch
+
+
+def load(import_torch: bool = True) -> C.CDLL:
+    """Loads (building first if needed) the HIP library; raises if impossible.
+
+    import_torch=False: for a process that never touches torch (the single-task
+    `hygeia infer`, which runs its chain through the host-pointer entry
+    hyg_tg_run_chain_host): torch's import (about 2 s of a fresh process) is
+    skipped. Such a process must not use torch's HIP afterwards (DeviceChains
+    refuses to)."""
+    global _lib, _with_torch
     if _lib is not None:
         return _lib
     # PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so) next to
     # the system one this library links. Both work in one process only when
     # torch's is initialised first, so torch is imported before our runtime
     # can initialise (it is the device-memory / stream plumbing anyway).
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    if import_torch:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    import sys
+
+    _with_torch = "torch" in sys.modules  # (its runtime loaded first, whoever imported it)
     path = os.environ.get("HYG_LIB_PATH", LIB_PATH)  # A/B builds of the same sources (tools/)
     if path == LIB_PATH and not os.path.exists(LIB_PATH):
         from . import build as _build

@@ -321,8 +321,12 @@ def _report_write_errors(writes) -> None:
 def _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c, nt_k, max_reads, ret, path, pool,
                 writes, log_z, times) -> None:
     """The chain runs of one `hygeia infer` task, one per --num_resampled_particles
-    value (run_inference_two_groups.py:263-322); result writes go to `pool`."""
-    from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
+    value (run_inference_two_groups.py:263-322); result writes go to `pool`.
+    The chain runs through the host-pointer entry, so this process never needs
+    torch: the library is loaded without it (a fresh task saves its import)."""
+    from . import _lib, two_group
+
+    _lib.load(import_torch=False)  # (raises without the HIP library)
 
     for M in f["num_resampled_particles"]:
         print(M)

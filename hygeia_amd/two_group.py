@@ -151,6 +151,10 @@ class DeviceChains:
                  device=None, final_weights: bool = False, workspace=None):
         import torch
 
+        if _lib.load() is not None and not _lib.loaded_with_torch():
+            raise RuntimeError("the HIP library was loaded without torch (import_torch=False): torch's HIP "
+                               "runtime must initialise first for device-tensor chains")
+
         self.torch = torch
         self.model = model
         self.device = device or torch.device("cuda", torch.cuda.current_device())

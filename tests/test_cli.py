@@ -209,3 +209,24 @@ def test_methylated_above_total_is_rejected(tmp_path, group, cmd):
         raise
     except Exception:
         pass
+
+
+def test_single_task_does_not_import_torch(tmp_path):
+    """A `hygeia infer` task runs its chain through the host-pointer C entry, so
+    its process never imports torch (about 2 s of every fresh task, which is
+    how modules/two_group/4_infer.nf runs it). Here, without a GPU, the task
+    stops at the device call; the check is on the process's modules."""
+    import subprocess
+    import sys
+
+    _write_inputs(str(tmp_path), "21", 300)
+    code = ("import sys\nfrom hygeia_amd import cli\n"
+            "try:\n    cli.main(sys.argv[1:])\nexcept Exception as e:\n    print('stopped:', type(e).__name__)\n"
+            "print('torch imported:', 'torch' in sys.modules)\n")
+    args = ["infer", "--chrom", "21", "--batch", "1", "--segment_size", "100", "--buffer_size", "10",
+            "--data_dir", str(tmp_path / "data"), "--single_group_dir", str(tmp_path / "sg"),
+            "--results_dir", str(tmp_path / "res")]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code] + args, capture_output=True, text=True, cwd=root,
+                       env=dict(os.environ, PYTHONPATH=root), timeout=300)
+    assert "torch imported: False" in r.stdout, r.stdout + r.stderr
