@@ -145,8 +145,9 @@ def serialize_flags(f: Dict[str, object]) -> str:
 
 # Wall-clock phase split of the last infer / infer_many call in this process
 # (seconds): parse (the chromosome's input files), device (model, chains, copies
-# back), writes (joining the result-file writes after the last chain). Read by
-# tools/bench_pipeline.py; nothing in the command's behaviour depends on it.
+# back), of which chains (the launches alone), writes (joining the result-file
+# writes after the last chain). Read by tools/bench_pipeline.py; nothing in the
+# command's behaviour depends on it.
 LAST_TIMINGS: Dict[str, float] = {}
 
 
@@ -343,6 +344,7 @@ def _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c,
         finally:
             model.close()
         times[N] = time.time() - t0
+        LAST_TIMINGS["chains"] = LAST_TIMINGS.get("chains", 0.0) + times[N]  # (inside "device")
         log_z[N] = float(ex["log_z"])
         pr = res.particle
         for name, arr in ((f"optimal_backward_particles_merged_state_{N}_{seed}",
@@ -475,6 +477,7 @@ def _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, 
         dc.run(E)
         torch.cuda.synchronize(dev)
         dt = time.time() - t0
+        LAST_TIMINGS["chains"] = LAST_TIMINGS.get("chains", 0.0) + dt  # (inside "device")
         status = dc.status.cpu().numpy()
         if (status != 0).any():
             from . import _lib

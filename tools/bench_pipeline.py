@@ -100,7 +100,7 @@ def main():
             raise RuntimeError(f"hygeia infer --batch {b} failed: {r.stderr[-2000:]}")
         split = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("@@")][-1][2:])
         one.append({"batch": b, "seed": sd, "process_wall_s": wall,
-                    "split_s": {k: split[k] for k in ("import_cli", "parse", "device", "writes", "main") if k in split}})
+                    "split_s": {k: split[k] for k in ("import_cli", "parse", "device", "chains", "writes", "main") if k in split}})
         print(f"task batch {b} seed {sd}: {wall:.1f} s {one[-1]['split_s']}", flush=True)
     t_one = sum(o["process_wall_s"] for o in one) / len(one)
     tasks = n_batches * len(seeds)
