@@ -115,6 +115,7 @@ class SgChain(C.Structure):
 EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy", "hyg_tg_num_particles",
            "hyg_tg_threads_per_chain", "hyg_tg_force_threads", "hyg_tg_chains_per_cu",
            "hyg_tg_emission", "hyg_tg_workspace_bytes", "hyg_tg_run_chains", "hyg_tg_run_chain_host",
+           "hyg_tg_run_chains_host",
            "hyg_device_count", "hyg_last_error", "hyg_version", "hyg_set_kernel_timing", "hyg_tg_last_kernel_ms",
            "hyg_sg_params_default", "hyg_sg_model_create", "hyg_sg_model_destroy", "hyg_sg_emission",
            "hyg_sg_workspace_bytes", "hyg_sg_run_chains", "hyg_sg_run_chain_host",
@@ -190,6 +191,9 @@ def load(import_torch: bool = True) -> C.CDLL:
     L.hyg_tg_run_chains.argtypes = [vp, C.POINTER(TgChain), i32, vp, vp, sz, C.POINTER(TgOutputs), vp]
     L.hyg_tg_run_chain_host.restype = C.c_int
     L.hyg_tg_run_chain_host.argtypes = [vp, vp, vp, i32, vp, vp, i32, i32, u64, u64, vp, vp, vp, vp, vp, vp, vp]
+    L.hyg_tg_run_chains_host.restype = C.c_int
+    L.hyg_tg_run_chains_host.argtypes = [vp, vp, vp, i32, vp, vp, i32, i64, C.POINTER(TgChain), i32, i64,
+                                         vp, vp, vp, vp, vp, vp, vp, vp]
     L.hyg_device_count.restype = C.c_int
     L.hyg_device_count.argtypes = []
     L.hyg_last_error.restype = C.c_char_p

@@ -218,21 +218,67 @@ def segment_index(n_sites: int, batch: int, segment_size: int, buffer_size: int)
     return (lo, hi), ret
 
 
+def _cpu_budget() -> int:
+    """CPUs this process may use: its affinity, capped by a cgroup-v2 CPU quota
+    (a container's affinity can list every core of the host)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+_POW10 = 10 ** np.arange(19, dtype=np.uint64)
+
+
+def _sci18_table(v: np.ndarray) -> np.ndarray:
+    """'%.18e' % float(x) of each integer x with |x| < 2**53, as an (n, 25)
+    uint8 table (a NUL in column 0 where there is no sign). float(x) is exact,
+    so its 19 significant digits are x's own digits followed by zeros and the
+    exponent is (number of digits - 1): built with array arithmetic, no Python
+    format call per value."""
+    v = v.astype(np.int64)
+    m = np.abs(v).astype(np.uint64)
+    e = (m[:, None] >= _POW10[None, 1:]).sum(axis=1)  # digits - 1 (0 for x == 0)
+    shift = e[:, None] - np.arange(19)[None, :]  # digit i (0 = leading) = m // 10**(e - i) % 10
+    dig = np.where(shift >= 0, (m[:, None] // _POW10[np.clip(shift, 0, 18)]) % np.uint64(10), 0).astype(np.uint8)
+    t = np.empty((v.shape[0], 25), np.uint8)
+    t[:, 0] = np.where(v < 0, ord("-"), 0)
+    t[:, 1] = 48 + dig[:, 0]
+    t[:, 2] = ord(".")
+    t[:, 3:21] = 48 + dig[:, 1:]
+    t[:, 21], t[:, 22] = ord("e"), ord("+")
+    t[:, 23], t[:, 24] = 48 + e // 10, 48 + e % 10
+    return t
+
+
 def _savetxt(path: str, a: np.ndarray) -> None:
     """np.savetxt(path, a, delimiter=",") (default fmt '%.18e', gzip by
     extension, as the reference writes these files) for integer-valued arrays:
-    the same text, formatted through a table of the distinct values instead of
-    a Python format call per element."""
+    the same text, built as bytes by array operations (_sci18_table of the
+    distinct values, gathered, separators added, sign padding dropped). The
+    batch input copies are written on a thread pool while the chains run: a
+    formatter that held the GIL per value or per row (np.savetxt, str.join)
+    starved the launching thread (11 s of a 14 s infer_many, profiles r04j)."""
     a = np.asarray(a)
-    if a.ndim not in (1, 2) or a.dtype.kind not in "iu" or a.size == 0:
+    if (a.ndim not in (1, 2) or a.dtype.kind not in "iu" or a.size == 0
+            or int(a.max()) >= 2 ** 53 or int(a.min()) <= -2 ** 53):
         np.savetxt(path, a, delimiter=",")
         return
-    vals, inv = np.unique(a, return_inverse=True)
-    txt = np.array(["%.18e" % float(v) for v in vals], dtype=object)[inv.reshape(a.shape)]
-    lines = txt if a.ndim == 1 else [",".join(r) for r in txt.tolist()]
-    body = ("\n".join(lines) + "\n").encode("latin-1")
+    a2 = a.reshape(a.shape[0], -1)
+    vals, inv = np.unique(a2, return_inverse=True)
+    buf = np.empty(a2.shape + (26,), np.uint8)
+    buf[..., :25] = _sci18_table(vals)[inv.reshape(a2.shape)]
+    buf[..., 25] = ord(",")
+    buf[:, -1, 25] = ord("\n")
+    flat = buf.reshape(-1)
+    body = flat[flat != 0].tobytes()
     if path.endswith(".gz"):
-        with gzip.open(path, "wb", compresslevel=6) as fh:  # zlib's default level (numpy's gzip: 9)
+        with gzip.open(path, "wb", compresslevel=3) as fh:  # same text; numpy's gzip level 9 is ~5x slower here
             fh.write(body)
     else:
         with open(path, "wb") as fh:
@@ -382,7 +428,7 @@ MANY_FLAGS = FLAGS_SPEC + [
 
 def infer_many(argv: Sequence[str]) -> int:
     """Multi-task `hygeia infer`: every (batch, seed) task of one chromosome in
-    ONE batched launch (hyg_tg_run_chains, one workgroup per chain), writing
+    ONE batched launch (hyg_tg_run_chains_host, one workgroup per chain, no torch), writing
     the same results_dir/chrom_{chrom}_{batch}/ files as the single-task runs
     `hygeia infer --batch b --seed s` that modules/two_group/4_infer.nf:42-48
     fans out (flags{seed}.txt as that run's flags, identical trajectories,
@@ -420,8 +466,9 @@ def infer_many(argv: Sequence[str]) -> int:
         return 0
     from concurrent.futures import ThreadPoolExecutor
 
-    pool = ThreadPoolExecutor(max_workers=max(1, min(16, len(os.sched_getaffinity(0)))))
-    writes = []
+    # one core stays with the thread that imports torch and launches the chains
+    pool = ThreadPoolExecutor(max_workers=max(1, min(16, _cpu_budget() - 1)))
+    writes, input_jobs = [], []
     for (b, lo, hi, r0, r1) in tasks:
         path = os.path.join(str(f["results_dir"]), "chrom_{}_{}".format(chrom, b))
         os.makedirs(path, exist_ok=True)
@@ -429,31 +476,35 @@ def infer_many(argv: Sequence[str]) -> int:
             fs = dict(f, batch=b, seed=sd)
             with open(os.path.join(path, f"flags{sd}.txt"), "w") as fh:
                 fh.write(serialize_flags(fs))
-        writes.append(pool.submit(_write_batch_inputs, path, meth_c[lo:hi], meth_k[lo:hi], tot_c[lo:hi],
-                                  tot_k[lo:hi], positions[lo:hi].astype(np.int64), slice(r0, r1)))
+        input_jobs.append((_write_batch_inputs, path, meth_c[lo:hi], meth_k[lo:hi], tot_c[lo:hi], tot_k[lo:hi],
+                           positions[lo:hi].astype(np.int64), slice(r0, r1)))
+
+    def submit_inputs():  # called just before the launch: the copies compress while the chains run
+        while input_jobs:
+            writes.append(pool.submit(*input_jobs.pop(0)))
 
     t_dev = time.perf_counter()
     try:
         return _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, meth_k, tot_k, pool,
-                               writes)
+                               writes, submit_inputs)
     finally:
         t_w = time.perf_counter()
         LAST_TIMINGS["device"] = t_w - t_dev  # (includes submitting the result writes)
+        submit_inputs()  # (no-op unless the device phase failed before its launch)
         for w in writes:  # zlib releases the GIL: the files compress in parallel
             w.result()
         pool.shutdown()
         LAST_TIMINGS["writes"] = time.perf_counter() - t_w
 
 
-def _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, meth_k, tot_k, pool, writes) -> int:
-    import torch
+def _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, meth_k, tot_k, pool, writes,
+                    submit_inputs) -> int:
+    from . import _lib, two_group
 
-    from . import two_group  # loads libhygeia_amd.so (raises without the HIP library)
-
-    dev = torch.device("cuda", torch.cuda.current_device())
+    # the batched host-pointer entry needs no torch (its import is ~2 s of a fresh process)
+    _lib.load(import_torch=False)  # (raises without the HIP library)
     lo_all, hi_all = min(t[1] for t in tasks), max(t[2] for t in tasks)
-    to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a[lo_all:hi_all], dtype=np.uint16).view(np.int16)).to(dev)  # noqa: E731
-    d_mc, d_tc, d_mk, d_tk = to_dev(meth_c), to_dev(tot_c), to_dev(meth_k), to_dev(tot_k)
+    counts = {k: a[lo_all:hi_all] for k, a in (("mc", meth_c), ("tc", tot_c), ("mk", meth_k), ("tk", tot_k))}
     max_reads = int(max(tot_c[lo_all:hi_all].max(initial=0), tot_k[lo_all:hi_all].max(initial=0)))
     chains, out = [], 0
     for (b, lo, hi, r0, r1) in tasks:
@@ -471,20 +522,20 @@ def _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, 
             num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
             max_total_reads=max_reads, max_duration=max(c[1] for c in chains) + 1,
             multinomial=bool(f["multinomial"]))
+        submit_inputs()  # the copies compress on the pool while the chains run (ctypes drops the GIL)
         t0 = time.time()
-        dc = two_group.DeviceChains(model, chains, out, device=dev)
-        E = dc.emission(d_mc, d_tc, d_mk, d_tk)
-        dc.run(E)
-        torch.cuda.synchronize(dev)
+        try:
+            r = two_group.run_chains_host({"control": counts["mc"], "case": counts["mk"]},
+                                          {"control": counts["tc"], "case": counts["tk"]}, model, chains, out)
+        finally:
+            model.close()
         dt = time.time() - t0
         LAST_TIMINGS["chains"] = LAST_TIMINGS.get("chains", 0.0) + dt  # (inside "device")
-        status = dc.status.cpu().numpy()
+        status = r["status"]
         if (status != 0).any():
-            from . import _lib
-
             raise _lib.HygError(int(status[status != 0][0]), "chains failed")
-        mg, ct, cs = dc.merged.cpu().numpy(), dc.control.cpu().numpy(), dc.case.cpu().numpy()
-        sp, rp, lz = dc.split_probs.cpu().numpy(), dc.regime_probs.cpu().numpy(), dc.log_z.cpu().numpy()
+        mg, ct, cs = r["merged"], r["control"], r["case"]
+        sp, rp, lz = r["split_probs"], r["regime_probs"], r["log_z"]
         i = 0
         for (b, lo, hi, r0, r1) in tasks:
             path = os.path.join(str(f["results_dir"]), "chrom_{}_{}".format(chrom, b))
@@ -500,7 +551,6 @@ def _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, 
                 log_z.setdefault((b, sd), {})[N] = float(lz[i])
                 times.setdefault((b, sd), {})[N] = dt * T / out  # the launch's wall time, pro rata
                 i += 1
-        model.close()
     for (b, sd), v in log_z.items():
         path = os.path.join(str(f["results_dir"]), "chrom_{}_{}".format(chrom, b))
         with open(os.path.join(path, f"log_normalizing_constants_optimal_{sd}.txt"), "w") as fh:

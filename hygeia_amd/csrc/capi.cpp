@@ -371,44 +371,51 @@ int hyg_tg_run_chains(const hyg_tg_model* m, const hyg_tg_chain* chains, int32_t
   return HYG_OK;
 }
 
-int hyg_tg_run_chain_host(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_t* tot_c, int32_t s_c,
-                          const uint16_t* meth_k, const uint16_t* tot_k, int32_t s_k, int32_t T, uint64_t seed,
-                          uint64_t chain_id, int16_t* merged, int16_t* control, int16_t* kase, float* split,
-                          float* regime, double* log_z, double* final_w) {
+int hyg_tg_run_chains_host(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_t* tot_c, int32_t s_c,
+                           const uint16_t* meth_k, const uint16_t* tot_k, int32_t s_k, int64_t n_sites,
+                           const hyg_tg_chain* chains, int32_t n_chains, int64_t out_rows, int16_t* merged,
+                           int16_t* control, int16_t* kase, float* split, float* regime, double* log_z,
+                           double* final_w, int32_t* status) {
   if (!m) return fail(HYG_EINVAL, "null model");
   if (!m->on_device) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
   if (!on_model_device(m->device)) return fail(HYG_EINVAL, "the current HIP device is not the model's device");
-  if (T < 1) return fail(HYG_EINVAL, "no sites");
-  for (int64_t i = 0; i < (int64_t)T * s_c; ++i)
+  if (n_sites < 1 || n_chains < 1 || out_rows < 1 || s_c < 0 || s_k < 0) return fail(HYG_EINVAL, "empty or negative size");
+  if (!chains || !merged || !control || !kase || !split || !regime || !log_z || !status)
+    return fail(HYG_EINVAL, "null argument");
+  if ((s_c && (!meth_c || !tot_c)) || (s_k && (!meth_k || !tot_k))) return fail(HYG_EINVAL, "null count buffer");
+  int64_t steps = 0;
+  for (int i = 0; i < n_chains; ++i) {
+    const hyg_tg_chain& c = chains[i];
+    if (c.n_sites < 1 || c.site_begin < 0 || c.out_begin < 0 || c.site_begin + c.n_sites > n_sites ||
+        c.out_begin + c.n_sites > out_rows)
+      return fail(HYG_EINVAL, "chain outside the sites or the output rows");
+    steps += c.n_sites;
+  }
+  for (int64_t i = 0; i < n_sites * s_c; ++i)
     if (meth_c[i] > tot_c[i] || tot_c[i] > m->nmax_reads) return fail(HYG_EINVAL, "invalid control counts");
-  for (int64_t i = 0; i < (int64_t)T * s_k; ++i)
+  for (int64_t i = 0; i < n_sites * s_k; ++i)
     if (meth_k[i] > tot_k[i] || tot_k[i] > m->nmax_reads) return fail(HYG_EINVAL, "invalid case counts");
-  const int K = m->c.K, B = m->c.B, Nmax = m->c.Nmax;
+  const size_t K = m->c.K, B = m->c.B, Nmax = m->c.Nmax, R = (size_t)out_rows, nch = (size_t)n_chains;
   struct Buf {
     void* p = nullptr;
     ~Buf() { if (p) (void)hipFree(p); }
   } b_mc, b_tc, b_mk, b_tk, b_E, b_ws, b_mg, b_ct, b_ks, b_sp, b_rp, b_lz, b_fw, b_st;
   auto alloc = [](Buf& b, size_t n) { return hipMalloc(&b.p, n ? n : 1) == hipSuccess; };
-  const size_t nc = (size_t)T * s_c, nk = (size_t)T * s_k;
-  const size_t wsb = hyg_tg_workspace_bytes(m, 1, T);
+  const size_t nc = (size_t)n_sites * s_c, nk = (size_t)n_sites * s_k;
+  const size_t wsb = hyg_tg_workspace_bytes(m, n_chains, steps);
   bool ok = alloc(b_mc, nc * 2) && alloc(b_tc, nc * 2) && alloc(b_mk, nk * 2) && alloc(b_tk, nk * 2) &&
-            alloc(b_E, sizeof(double) * T * 2 * K) && alloc(b_ws, wsb) && alloc(b_mg, 2 * (size_t)T * B) &&
-            alloc(b_ct, 4 * (size_t)T * B) && alloc(b_ks, 4 * (size_t)T * B) && alloc(b_sp, 4 * (size_t)T) &&
-            alloc(b_rp, 4 * (size_t)T * 2 * K) && alloc(b_lz, 8) && alloc(b_fw, 8 * (size_t)Nmax) && alloc(b_st, 4);
+            alloc(b_E, sizeof(double) * (size_t)n_sites * 2 * K) && alloc(b_ws, wsb) && alloc(b_mg, 2 * R * B) &&
+            alloc(b_ct, 4 * R * B) && alloc(b_ks, 4 * R * B) && alloc(b_sp, 4 * R) && alloc(b_rp, 4 * R * 2 * K) &&
+            alloc(b_lz, 8 * nch) && (!final_w || alloc(b_fw, 8 * nch * Nmax)) && alloc(b_st, 4 * nch);
   if (!ok) return fail(HYG_ENOMEM, "device allocation failed");
-  if (hipMemcpy(b_mc.p, meth_c, nc * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(b_tc.p, tot_c, nc * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(b_mk.p, meth_k, nk * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(b_tk.p, tot_k, nk * 2, hipMemcpyHostToDevice) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  int rc = hyg_tg_emission(m, (uint16_t*)b_mc.p, (uint16_t*)b_tc.p, s_c, (uint16_t*)b_mk.p, (uint16_t*)b_tk.p, s_k, T,
-                           (double*)b_E.p, nullptr);
+  auto h2d = [](void* d, const void* h, size_t n) { return n == 0 || hipMemcpy(d, h, n, hipMemcpyHostToDevice) == hipSuccess; };
+  auto d2h = [](void* h, const void* d, size_t n) { return hipMemcpy(h, d, n, hipMemcpyDeviceToHost) == hipSuccess; };
+  if (!h2d(b_mc.p, meth_c, nc * 2) || !h2d(b_tc.p, tot_c, nc * 2) || !h2d(b_mk.p, meth_k, nk * 2) ||
+      !h2d(b_tk.p, tot_k, nk * 2))
+    return fail(HYG_EDEVICE, "copy failed");
+  int rc = hyg_tg_emission(m, (uint16_t*)b_mc.p, (uint16_t*)b_tc.p, s_c, (uint16_t*)b_mk.p, (uint16_t*)b_tk.p, s_k,
+                           n_sites, (double*)b_E.p, nullptr);
   if (rc) return rc;
-  hyg_tg_chain ch{};
-  ch.site_begin = 0;
-  ch.n_sites = T;
-  ch.seed = seed;
-  ch.chain_id = chain_id;
-  ch.out_begin = 0;
   hyg_tg_outputs o{};
   o.merged = (int16_t*)b_mg.p;
   o.control = (int16_t*)b_ct.p;
@@ -418,18 +425,31 @@ int hyg_tg_run_chain_host(const hyg_tg_model* m, const uint16_t* meth_c, const u
   o.log_z = (double*)b_lz.p;
   o.final_log_weights = (double*)b_fw.p;
   o.status = (int32_t*)b_st.p;
-  rc = hyg_tg_run_chains(m, &ch, 1, (double*)b_E.p, b_ws.p, wsb, &o, nullptr);
+  rc = hyg_tg_run_chains(m, chains, n_chains, (double*)b_E.p, b_ws.p, wsb, &o, nullptr);
   if (rc) return rc;
   if (hipDeviceSynchronize() != hipSuccess) return fail(HYG_EDEVICE, "kernel execution failed");
-  int32_t st = 0;
-  if (hipMemcpy(&st, b_st.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(merged, b_mg.p, 2 * (size_t)T * B, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(control, b_ct.p, 4 * (size_t)T * B, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(kase, b_ks.p, 4 * (size_t)T * B, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(split, b_sp.p, 4 * (size_t)T, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(regime, b_rp.p, 4 * (size_t)T * 2 * K, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (hipMemcpy(log_z, b_lz.p, 8, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
-  if (final_w && hipMemcpy(final_w, b_fw.p, 8 * (size_t)Nmax, hipMemcpyDeviceToHost) != hipSuccess) return fail(HYG_EDEVICE, "copy failed");
+  if (!d2h(status, b_st.p, 4 * nch) || !d2h(merged, b_mg.p, 2 * R * B) || !d2h(control, b_ct.p, 4 * R * B) ||
+      !d2h(kase, b_ks.p, 4 * R * B) || !d2h(split, b_sp.p, 4 * R) || !d2h(regime, b_rp.p, 4 * R * 2 * K) ||
+      !d2h(log_z, b_lz.p, 8 * nch) || (final_w && !d2h(final_w, b_fw.p, 8 * nch * Nmax)))
+    return fail(HYG_EDEVICE, "copy failed");
+  return HYG_OK;
+}
+
+int hyg_tg_run_chain_host(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_t* tot_c, int32_t s_c,
+                          const uint16_t* meth_k, const uint16_t* tot_k, int32_t s_k, int32_t T, uint64_t seed,
+                          uint64_t chain_id, int16_t* merged, int16_t* control, int16_t* kase, float* split,
+                          float* regime, double* log_z, double* final_w) {
+  if (T < 1) return fail(HYG_EINVAL, "no sites");
+  hyg_tg_chain ch{};
+  ch.site_begin = 0;
+  ch.n_sites = T;
+  ch.seed = seed;
+  ch.chain_id = chain_id;
+  ch.out_begin = 0;
+  int32_t st = HYG_OK;
+  const int rc = hyg_tg_run_chains_host(m, meth_c, tot_c, s_c, meth_k, tot_k, s_k, T, &ch, 1, T, merged, control, kase,
+                                        split, regime, log_z, final_w, &st);
+  if (rc) return rc;
   if (st != HYG_OK) return fail(st, "all particle weights became -inf");
   return HYG_OK;
 }

@@ -136,6 +136,41 @@ def run(observations: Dict[str, np.ndarray], n_total_reads: Dict[str, np.ndarray
     return res, final_w, {"split_probs": split, "regime_probs": regime, "log_z": log_z.value}
 
 
+def run_chains_host(observations: Dict[str, np.ndarray], n_total_reads: Dict[str, np.ndarray],
+                    model: CaseControlModel, chains: List[Tuple[int, int, int, int, int]], n_out_rows: int,
+                    final_weights: bool = False) -> Dict[str, np.ndarray]:
+    """Many chains in one launch from host arrays (hyg_tg_run_chains_host), with
+    no torch: `hygeia infer_many`'s every (batch, seed) task of a chromosome.
+    chains: (site_begin, n_sites, seed, chain_id, out_begin) over the count rows
+    and the output rows. Returns host arrays: merged [R,B], control / case
+    [R,B,2], split_probs [R], regime_probs [R,2K], log_z / status [n_chains]
+    (and final_w [n_chains, N_max]); each chain's rows are those of run()."""
+    mc, tc = _u16(observations["control"]), _u16(n_total_reads["control"])
+    mk, tk = _u16(observations["case"]), _u16(n_total_reads["case"])
+    T = tc.shape[0]
+    if mc.shape != tc.shape or mk.shape != tk.shape or tk.shape[0] != T:
+        raise ValueError("inconsistent count shapes")
+    if max(int(c[1]) for c in chains) > model.max_duration:
+        raise ValueError(f"a chain exceeds the model's max_duration {model.max_duration}")
+    arr = (_lib.TgChain * len(chains))()
+    for i, (site_begin, n_sites, seed, chain_id, out_begin) in enumerate(chains):
+        arr[i].site_begin, arr[i].n_sites = int(site_begin), int(n_sites)
+        arr[i].seed, arr[i].chain_id, arr[i].out_begin = int(seed), int(chain_id), int(out_begin)
+    K, B, R, n = model.n_regimes, model.num_samples_backward, int(n_out_rows), len(chains)
+    out = {"merged": np.empty((R, B), np.int16), "control": np.empty((R, B, 2), np.int16),
+           "case": np.empty((R, B, 2), np.int16), "split_probs": np.empty(R, np.float32),
+           "regime_probs": np.empty((R, 2 * K), np.float32), "log_z": np.empty(n, np.float64),
+           "status": np.empty(n, np.int32)}
+    if final_weights:
+        out["final_w"] = np.empty((n, model.num_particles), np.float64)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    _lib.check(_lib.load().hyg_tg_run_chains_host(
+        model.handle, p(mc), p(tc), mc.shape[1], p(mk), p(tk), mk.shape[1], T, arr, n, R, p(out["merged"]),
+        p(out["control"]), p(out["case"]), p(out["split_probs"]), p(out["regime_probs"]), p(out["log_z"]),
+        p(out["final_w"]) if final_weights else None, p(out["status"])))
+    return out
+
+
 class DeviceChains:
     """Batched device-resident execution of many chains (the bench and the
     multi-chain driver): emission table, history workspace and outputs are

@@ -176,6 +176,21 @@ int hyg_tg_run_chain_host(const hyg_tg_model* model, const uint16_t* meth_ctrl, 
                           int16_t* kase, float* split_probs, float* regime_probs, double* log_z,
                           double* final_log_weights);
 
+/* Host-pointer form of hyg_tg_run_chains (round 4): the counts of n_sites
+ * sites (host, site-major) are copied in, the emission table is formed, the
+ * n_chains chains (host array: site_begin into the counts, out_begin into the
+ * output rows) run in one launch, and the outputs come back into host arrays
+ * of out_rows rows (layouts as above), log_z and status [n_chains]
+ * (final_log_weights [n_chains][N_max], may be NULL). Returns HYG_OK when the
+ * launch ran; a chain whose weights all became -inf has HYG_ENUMERIC in its
+ * status. `hygeia infer_many` (every task that modules/two_group/4_infer.nf:42-48
+ * fans out, in one launch) runs through it without torch. */
+int hyg_tg_run_chains_host(const hyg_tg_model* model, const uint16_t* meth_ctrl, const uint16_t* tot_ctrl,
+                           int32_t s_ctrl, const uint16_t* meth_case, const uint16_t* tot_case, int32_t s_case,
+                           int64_t n_sites, const hyg_tg_chain* chains, int32_t n_chains, int64_t out_rows,
+                           int16_t* merged, int16_t* control, int16_t* kase, float* split_probs,
+                           float* regime_probs, double* log_z, double* final_log_weights, int32_t* status);
+
 /* Kernel timing for benchmarks: when enabled, HIP events are recorded on the
  * launch stream around the emission, forward and backward kernels;
  * hyg_tg_last_kernel_ms waits for the last ones and returns their durations

@@ -149,6 +149,28 @@ def test_fast_savetxt_matches_numpy(tmp_path, shape, dtype):
     assert (tmp_path / "c.csv").read_bytes() == (tmp_path / "d.csv").read_bytes()
 
 
+def test_sci18_table_matches_format():
+    """The array-built '%.18e' text equals Python's for every digit count and
+    sign, up to 2**53 - 1 (positions, counts, negative sentinels)."""
+    edge = [0, 1, -1, 9, 10, -10, 99, 100, 2 ** 31 - 1, -2 ** 31, 2 ** 53 - 1, -(2 ** 53 - 1)]
+    edge += [s * (10 ** k + d) for k in range(16) for d in (-1, 0, 1) for s in (1, -1)]
+    rnd = np.random.default_rng(5).integers(-2 ** 53 + 1, 2 ** 53, size=20000)
+    vals = np.concatenate([np.array(edge, np.int64), rnd, (rnd % 1000003)])
+    t = cli._sci18_table(vals)
+    got = [bytes(r[r != 0]).decode() for r in t]
+    assert got == ["%.18e" % float(v) for v in vals]
+
+
+@pytest.mark.parametrize("dtype", [np.int64, np.uint64, np.uint8])
+def test_fast_savetxt_wide_and_unsigned(tmp_path, dtype):
+    """Values at the 2**53 edge and unsigned types: the same text as np.savetxt."""
+    info = np.iinfo(dtype)
+    a = np.array([[0, 1], [info.max, 7], [min(info.max, 2 ** 53 - 1), 3]], dtype=dtype)
+    cli._savetxt(str(tmp_path / "c.csv"), a)
+    np.savetxt(str(tmp_path / "d.csv"), a, delimiter=",")
+    assert (tmp_path / "c.csv").read_bytes() == (tmp_path / "d.csv").read_bytes()
+
+
 def test_read_matrix_equals_pandas(tmp_path):
     """cli._read_matrix (pyarrow, pandas re-read for non-integral input) gives
     pandas' values (the reference's parser, run_inference_two_groups.py:177-191)

@@ -204,6 +204,43 @@ def test_batched_chains_and_emission(oracle):
         np.testing.assert_array_equal(dc.final_w[i].cpu().numpy(), ref["final_log_weights"])
 
 
+def test_batched_host_entry(oracle):
+    """hyg_tg_run_chains_host (infer_many's torch-free launch): overlapping
+    chains over one count range (segments with buffers, two seeds), outputs
+    in any row order; each chain equals its own oracle run. Bad chain ranges
+    and counts are refused before anything runs."""
+    from hygeia_amd import _lib, two_group
+
+    K, M, B, S = 6, 50, 25, 4
+    mu, sg, theta, d, p = _setup(oracle, K, M, B, 3000, S, 100.0, 33)
+    obs = {"control": d["meth_control"], "case": d["meth_case"]}
+    tot = {"control": d["tot_control"], "case": d["tot_case"]}
+    spans = [(0, 1200), (800, 1400), (1800, 1200), (2999, 1)]  # (site_begin, n_sites)
+    chains, out = [], 0
+    for j, (s0, n) in enumerate(reversed(spans)):  # output rows in reverse site order
+        for seed in (0, 1):
+            chains.append((s0, n, seed, 4000 + j, out))
+            out += n
+    model = _model(mu, sg, theta, M, B, int(max(d["tot_control"].max(), d["tot_case"].max())), 1500)
+    r = two_group.run_chains_host(obs, tot, model, chains, out + 7, final_weights=True)
+    assert (r["status"] == 0).all()
+    E_ref = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    for i, (s0, n, seed, cid, o0) in enumerate(chains):
+        ref = oracle.chain(p, E_ref[s0:s0 + n], seed, cid)
+        for k, rk in (("merged", "merged"), ("control", "control"), ("case", "case"),
+                      ("split_probs", "split_probs"), ("regime_probs", "regime_probs")):
+            np.testing.assert_array_equal(r[k][o0:o0 + n], ref[rk])
+        assert r["log_z"][i] == ref["log_z"]
+        np.testing.assert_array_equal(r["final_w"][i], ref["final_log_weights"])
+    for bad in ([(2500, 600, 0, 1, 0)], [(0, 100, 0, 1, out)]):  # past the sites / past the output rows
+        with pytest.raises(_lib.HygError):
+            two_group.run_chains_host(obs, tot, model, bad, out)
+    m2 = {k: v.copy() for k, v in obs.items()}
+    m2["case"][5, 0] = tot["case"][5, 0] + 1
+    with pytest.raises(_lib.HygError):
+        two_group.run_chains_host(m2, tot, model, chains[:1], out)
+
+
 def test_long_chain_properties_and_determinism():
     """A full-length segment chain (110k sites, the reference's segment +
     buffers): size-independent properties, and bit-identical reruns."""
