@@ -164,9 +164,8 @@ def _read_matrix(path: str) -> np.ndarray:
     files hold integer counts (plain or '%.18e' text), which every correct
     parser reads exactly, so the values equal pandas'; a matrix with any
     non-integral or non-finite value (or one pyarrow cannot read) is re-read
-    with pandas, the reference's parser, so such input keeps its exact values."""
-    import pandas as pd
-
+    with pandas, the reference's parser, so such input keeps its exact values.
+    (pandas is imported on that path only.)"""
     try:
         import pyarrow.csv as pacsv
 
@@ -179,6 +178,8 @@ def _read_matrix(path: str) -> np.ndarray:
                 return a
     except Exception:  # noqa: BLE001 -- any pyarrow failure (ArrowInvalid, ArrowNotImplementedError,
         pass  # ArrowTypeError, ...) falls back to pandas, the reference's parser
+    import pandas as pd
+
     return pd.read_csv(path, sep=",", header=None, dtype=np.float64).to_numpy()
 
 
@@ -197,7 +198,11 @@ def _read_inputs(data_dir: str, chrom: str):
 
 
 def read_theta(single_group_dir: str, chrom: str) -> np.ndarray:
-    """theta_{chrom}.csv.gz, column 'data' (run_inference_two_groups.py:76-79)."""
+    """theta_{chrom}.csv.gz, column 'data' (run_inference_two_groups.py:76-79),
+    read by pandas as the reference reads it: pandas' default float converter
+    is not Python's float() (it drops digits past the 17th character of the
+    mantissa, leading zeros included: tests/test_cli.py::test_read_theta_equals_pandas),
+    and theta's bits set every transition probability."""
     import pandas as pd
 
     df = pd.read_table(os.path.join(single_group_dir, f"theta_{chrom}.csv.gz"), sep=",")

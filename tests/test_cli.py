@@ -149,6 +149,37 @@ def test_fast_savetxt_matches_numpy(tmp_path, shape, dtype):
     assert (tmp_path / "c.csv").read_bytes() == (tmp_path / "d.csv").read_bytes()
 
 
+@pytest.mark.parametrize("form", ["repr", "%.18e", "%.6g", "quoted_header", "index_col", "int", "odd"])
+def test_read_theta_equals_pandas(tmp_path, form):
+    """read_theta gives pandas' values, the reference's reader
+    (run_inference_two_groups.py:76-79), on every text form; on 17-digit repr
+    text those differ from Python's correctly rounded float()."""
+    import pandas as pd
+
+    v = np.random.default_rng(7).normal(0.0, 3.0, size=42) * 10.0 ** np.random.default_rng(8).integers(-12, 12, 42)
+    fmt = {"repr": repr, "%.18e": lambda x: "%.18e" % x, "%.6g": lambda x: "%.6g" % x}.get(form, repr)
+    body = [fmt(float(x)) for x in v]
+    if form == "quoted_header":
+        text = '"data"\n' + "\n".join(body) + "\n"
+    elif form == "index_col":
+        text = ",data\n" + "\n".join(f"{i},{b}" for i, b in enumerate(body)) + "\n"
+    elif form == "int":
+        text = "data\n" + "\n".join(str(i - 20) for i in range(42)) + "\n"
+    elif form == "odd":  # a blank, a NaN spelling and an empty line: the pandas path
+        text = "data\n" + "\n".join(body[:5]) + "\n 1.5\nNA\n\n" + "\n".join(body[5:]) + "\n"
+    else:
+        text = "data\n" + "\n".join(body) + "\n"
+    d = tmp_path / "sg"
+    d.mkdir()
+    with gzip.open(d / "theta_7.csv.gz", "wt") as fh:
+        fh.write(text)
+    got = cli.read_theta(str(d), "7")
+    want = pd.to_numeric(pd.read_table(d / "theta_7.csv.gz", sep=",")["data"]).to_numpy(dtype=np.float64)
+    np.testing.assert_array_equal(got, want)
+    if form == "repr":  # why the reader stays pandas: its converter is not float()'s on such text
+        assert not np.array_equal(want, np.array([float(b) for b in body]))
+
+
 def test_sci18_table_matches_format():
     """The array-built '%.18e' text equals Python's for every digit count and
     sign, up to 2**53 - 1 (positions, counts, negative sentinels)."""
