@@ -304,6 +304,10 @@ int32_t hyg_tg_chains_per_cu(const hyg_tg_model* m, int32_t n_chains) {
   return hyg::tg_resident_per_cu(m->c, n_chains);
 }
 
+size_t hyg_tg_lds_bytes(const hyg_tg_model* m, int32_t threads, int32_t backward) {
+  return m ? hyg::tg_layout_bytes(m->c, threads, backward != 0) : 0;
+}
+
 int hyg_tg_force_threads(int32_t forward, int32_t backward) {
   const int rc = hyg::tg_force_threads(forward, backward);
   return rc == HYG_OK ? rc : fail(rc, "unsupported workgroup size");

@@ -79,5 +79,6 @@ size_t backward_lds_bytes(const hyg_tg_consts& c, int n_chains);
 int tg_threads_per_chain(const hyg_tg_consts& c, int n_chains);  // forward workgroup size of a launch
 int tg_force_threads(int fwd, int bwd);                           // test override (0 = automatic)
 int tg_resident_per_cu(const hyg_tg_consts& c, int n_chains);     // forward workgroups per CU
+size_t tg_layout_bytes(const hyg_tg_consts& c, int threads, bool backward);  // LDS of one chain (0: bad width)
 
 }  // namespace hyg

@@ -2726,6 +2726,9 @@ int last_kernel_ms(float* out3) {
 size_t forward_lds_bytes(const hyg_tg_consts& c, int n_chains) {
   return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(false, c, n_chains), false).total;
 }
+size_t tg_layout_bytes(const hyg_tg_consts& c, int threads, bool backward) {
+  return valid_width(threads) ? make_layout(c.K, c.M, c.B, c.Nmax, threads, backward).total : 0;
+}
 size_t backward_lds_bytes(const hyg_tg_consts& c, int n_chains) {
   return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(true, c, n_chains), true).total;
 }

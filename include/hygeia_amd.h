@@ -121,6 +121,14 @@ int32_t hyg_tg_threads_per_chain(const hyg_tg_model* model, int32_t n_chains);
  * device. Diagnostic. */
 int32_t hyg_tg_chains_per_cu(const hyg_tg_model* model, int32_t n_chains);
 
+/* LDS bytes of one chain workgroup of the forward (backward = 0) or backward
+ * kernel at `threads` (64, 128, 256, 512 or 768; 0 for another width). No
+ * device needed. Diagnostic: C3 on one GPU needs three 256-thread forward
+ * chains per CU, and the hardware's LDS allocation leaves the pipeline shape
+ * little room (53 520 B holds three per CU; 53 776 B held two while the
+ * occupancy query still reported three); tests pin it. */
+size_t hyg_tg_lds_bytes(const hyg_tg_model* model, int32_t threads, int32_t backward);
+
 /* Test / tuning override of the chain workgroup sizes for every later launch
  * in the process: forward and backward threads (64, 128, 256, 512 or 768;
  * 0 = the automatic choice above). Not thread-safe. The results do not depend

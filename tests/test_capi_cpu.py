@@ -103,6 +103,32 @@ def test_compute_refuses_without_device(lib):
         E = np.zeros((T, 12))
         rc = lib.hyg_tg_emission(m, ptr(z), ptr(z), 2, ptr(z), ptr(z), 2, T, ptr(E), None)
         assert rc == _lib.HYG_EDEVICE
+        ch = (_lib.TgChain * 1)()
+        ch[0].n_sites = T
+        st = np.zeros(1, np.int32)
+        rc = lib.hyg_tg_run_chains_host(m, ptr(z), ptr(z), 2, ptr(z), ptr(z), 2, T, ch, 1, T, ptr(out["mg"]),
+                                        ptr(out["ct"]), ptr(out["ks"]), ptr(out["sp"]), ptr(out["rp"]),
+                                        ptr(out["lz"]), None, ptr(st))
+        assert rc == _lib.HYG_EDEVICE
+    finally:
+        lib.hyg_tg_model_destroy(m)
+
+
+def test_pipeline_shape_lds_stays_under_the_three_per_cu_boundary(lib):
+    """C3 on one GPU holds three 256-thread forward chains per CU. The forward's
+    LDS at the pipeline shape (K = 6, M = 50, B = 25) is 53 520 B, which fits three
+    times; 256 B more (53 776 B) measured two per CU on the MI355X while the HIP
+    occupancy query still said three (C3 forward 1957 -> 2887 ms, profiles/r04s).
+    Growing the 256-thread layout needs a GPU check of C3 first."""
+    m = C.c_void_p()
+    assert lib.hyg_tg_model_create(C.byref(_params()), 200, 1000, C.byref(m)) == _lib.HYG_OK
+    try:
+        fwd256 = lib.hyg_tg_lds_bytes(m, 256, 0)
+        assert 0 < fwd256 <= 53520
+        assert 3 * lib.hyg_tg_lds_bytes(m, 256, 1) <= 160 * 1024  # the backward at three per CU
+        for nt in (512, 768):  # one chain per CU
+            assert 0 < lib.hyg_tg_lds_bytes(m, nt, 0) <= 160 * 1024
+        assert lib.hyg_tg_lds_bytes(m, 300, 0) == 0 and lib.hyg_tg_lds_bytes(None, 256, 0) == 0
     finally:
         lib.hyg_tg_model_destroy(m)
 
