@@ -2323,7 +2323,22 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
           // point when dcn = 1) can reach xn: lc of tg_trans is a constant -inf
           // otherwise (ancestors always have d_c >= 1).
           int r0a, r0b, r1a, r1b;
-          if (dcn >= 3) { r0a = 0; r0b = 1; r1a = K; r1b = 2 * K; }                         // A, C, D
+          if (dcn >= 3) {  // A, C, D; the case side of trans_possible leaves fewer:
+            r0a = 0; r0b = 1; r1a = K; r1b = 2 * K;
+            if (mn == 1 && cl.u > 1) {
+              r1a = 2 * K - 1;  // D: a C child (m = 0, d_k = 1 < u) cannot merge
+            } else if (mn == 0 && dkn >= 2) {
+              // unmerged xn continuing its case segment: x.m = 0 (no D), x.d_k =
+              // d_k' - 1 and x.r_k = r_k' (a C child has d_k = 1, r_k = its slot's
+              // regime; candidates have r_c = r_c' as lc requires)
+              if (dkn == 2 && rkn != rcn) {
+                r1a = K + (rkn < rcn ? rkn : rkn - 1);
+                r1b = r1a + 1;
+              } else {
+                r1a = r1b = 2 * K;
+              }
+            }
+          }
           else if (dcn == 2) { r0a = 1; r0b = K; r1a = 2 * K + rcn * K; r1b = r1a + K; }   // B, E(i = rcn)
           else { r0a = 0; r0b = I; r1a = I; r1b = I; }
           const int nseg0 = r0b - r0a;
