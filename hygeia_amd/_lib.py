@@ -116,7 +116,8 @@ EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy
            "hyg_tg_threads_per_chain", "hyg_tg_force_threads", "hyg_tg_chains_per_cu", "hyg_tg_lds_bytes",
            "hyg_tg_emission", "hyg_tg_workspace_bytes", "hyg_tg_run_chains", "hyg_tg_run_chain_host",
            "hyg_tg_run_chains_host",
-           "hyg_device_count", "hyg_last_error", "hyg_version", "hyg_set_kernel_timing", "hyg_tg_last_kernel_ms",
+           "hyg_device_count", "hyg_device_slot_acquire", "hyg_device_slot_release", "hyg_set_device",
+           "hyg_get_device", "hyg_last_error", "hyg_version", "hyg_set_kernel_timing", "hyg_tg_last_kernel_ms",
            "hyg_sg_params_default", "hyg_sg_model_create", "hyg_sg_model_destroy", "hyg_sg_emission",
            "hyg_sg_workspace_bytes", "hyg_sg_run_chains", "hyg_sg_run_chain_host",
            "hyg_sg_pe_params_default", "hyg_sg_pe_theta_rows", "hyg_sg_pe_workspace_bytes", "hyg_sg_run_chains_pe",
@@ -198,6 +199,14 @@ def load(import_torch: bool = True) -> C.CDLL:
                                          vp, vp, vp, vp, vp, vp, vp, vp]
     L.hyg_device_count.restype = C.c_int
     L.hyg_device_count.argtypes = []
+    L.hyg_device_slot_acquire.restype = C.c_int
+    L.hyg_device_slot_acquire.argtypes = [C.c_char_p, i32, i32, C.POINTER(i32), C.POINTER(i32)]
+    L.hyg_device_slot_release.restype = C.c_int
+    L.hyg_device_slot_release.argtypes = []
+    L.hyg_set_device.restype = C.c_int
+    L.hyg_set_device.argtypes = [i32]
+    L.hyg_get_device.restype = C.c_int
+    L.hyg_get_device.argtypes = []
     L.hyg_last_error.restype = C.c_char_p
     L.hyg_last_error.argtypes = []
     L.hyg_set_kernel_timing.restype = None

@@ -358,6 +358,23 @@ def infer(argv: Sequence[str]) -> int:
     return 0
 
 
+# (device, slot) the last infer / infer_many call in this process ran on
+# (parallel.task_device); read by tests and tools/bench_pipeline.py.
+LAST_DEVICE: Dict[str, int] = {}
+
+
+def _use_task_device(L) -> None:
+    """Selects this task's GPU by the node policy of parallel.task_device (the
+    executor's device variables, else a per-node slot over every visible GPU)."""
+    from . import _lib, parallel
+
+    dev, slot = parallel.task_device(L)
+    if dev != 0 or slot >= 0:
+        _lib.check(L.hyg_set_device(dev))
+    LAST_DEVICE.clear()
+    LAST_DEVICE.update(device=dev, slot=slot)
+
+
 def _report_write_errors(writes) -> None:
     """On a failed run: wait for the result writes already submitted and report
     any of them that failed too (the run's own exception is the one raised)."""
@@ -378,7 +395,7 @@ def _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c,
     torch: the library is loaded without it (a fresh task saves its import)."""
     from . import _lib, two_group
 
-    _lib.load(import_torch=False)  # (raises without the HIP library)
+    _use_task_device(_lib.load(import_torch=False))  # (raises without the HIP library)
 
     for M in f["num_resampled_particles"]:
         print(M)
@@ -471,7 +488,7 @@ def infer_many(argv: Sequence[str]) -> int:
         return 0
     from concurrent.futures import ThreadPoolExecutor
 
-    # one core stays with the thread that imports torch and launches the chains
+    # one core stays with the thread that launches the chains (ctypes) and collects their outputs
     pool = ThreadPoolExecutor(max_workers=max(1, min(16, _cpu_budget() - 1)))
     writes, input_jobs = [], []
     for (b, lo, hi, r0, r1) in tasks:
@@ -507,7 +524,7 @@ def _infer_many_run(f, chrom, seeds, K, mu, sigma, theta, tasks, meth_c, tot_c, 
     from . import _lib, two_group
 
     # the batched host-pointer entry needs no torch (its import is ~2 s of a fresh process)
-    _lib.load(import_torch=False)  # (raises without the HIP library)
+    _use_task_device(_lib.load(import_torch=False))  # (raises without the HIP library)
     lo_all, hi_all = min(t[1] for t in tasks), max(t[2] for t in tasks)
     counts = {k: a[lo_all:hi_all] for k, a in (("mc", meth_c), ("tc", tot_c), ("mk", meth_k), ("tk", tot_k))}
     max_reads = int(max(tot_c[lo_all:hi_all].max(initial=0), tot_k[lo_all:hi_all].max(initial=0)))

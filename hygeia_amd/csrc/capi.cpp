@@ -2,8 +2,12 @@
 // tables, upload), workspace planning, chain descriptors, launches. Compiled by
 // hipcc into hygeia_amd/lib/libhygeia_amd.so together with tg_kernels.hip.
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -33,6 +37,10 @@ using namespace hyg;
 namespace {
 
 thread_local std::string g_err;
+
+// the process's device slot (hyg_device_slot_acquire): the descriptor holding the flock
+std::mutex g_slot_mu;
+int g_slot_fd = -1, g_slot_device = -1, g_slot_index = -1;
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -213,6 +221,65 @@ int hyg_device_count(void) {
     return 0;
   }
   return n;
+}
+
+int hyg_device_slot_acquire(const char* lock_dir, int32_t n_devices, int32_t max_per_device, int32_t* device,
+                            int32_t* slot) {
+  if (!lock_dir || !device || !slot) return fail(HYG_EINVAL, "null argument");
+  if (n_devices < 1 || max_per_device < 1) return fail(HYG_EINVAL, "n_devices and max_per_device must be >= 1");
+  std::lock_guard<std::mutex> g(g_slot_mu);
+  if (g_slot_fd >= 0) {  // one slot per process
+    *device = g_slot_device;
+    *slot = g_slot_index;
+    return HYG_OK;
+  }
+  for (int j = 0; j < max_per_device; ++j) {
+    for (int d = 0; d < n_devices; ++d) {
+      const std::string path =
+          std::string(lock_dir) + "/hygeia_amd.gpu" + std::to_string(d) + ".slot" + std::to_string(j) + ".lock";
+      int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+      if (fd < 0 && errno == EACCES) fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);  // another user's file
+      if (fd < 0) return fail(HYG_EINVAL, "device slot lock " + path + ": " + std::strerror(errno));
+      if (::flock(fd, LOCK_EX | LOCK_NB) == 0) {
+        g_slot_fd = fd;
+        g_slot_device = d;
+        g_slot_index = j;
+        *device = d;
+        *slot = j;
+        return HYG_OK;
+      }
+      const int err = errno;
+      ::close(fd);
+      if (err != EWOULDBLOCK) return fail(HYG_EINVAL, "device slot lock " + path + ": " + std::strerror(err));
+    }
+  }
+  return fail(HYG_EINVAL, "every device slot is held");
+}
+
+int hyg_device_slot_release(void) {
+  std::lock_guard<std::mutex> g(g_slot_mu);
+  if (g_slot_fd >= 0) ::close(g_slot_fd);  // closing the only descriptor drops the flock
+  g_slot_fd = -1;
+  g_slot_device = g_slot_index = -1;
+  return HYG_OK;
+}
+
+int hyg_set_device(int32_t device) {
+  const int n = hyg_device_count();
+  if (n < 1) return fail(HYG_EDEVICE, "no HIP device");
+  if (device < 0 || device >= n) return fail(HYG_EINVAL, "device out of range");
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return fail(HYG_EDEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  return HYG_OK;
+}
+
+int hyg_get_device(void) {
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(HYG_EDEVICE, "no HIP device");
+  }
+  return d;
 }
 
 void hyg_tg_params_default(hyg_tg_params* p) {

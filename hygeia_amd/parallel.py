@@ -15,6 +15,7 @@ the CPU tests drive the same code with "gloo".
 """
 from __future__ import annotations
 
+import os
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -70,3 +71,49 @@ def allreduce_counts(counts, always: bool = False):
     if dist.is_available() and dist.is_initialized() and (always or dist.get_world_size() > 1):
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
     return counts
+
+
+# Environment variables through which an executor assigns GPUs to a task; when
+# any is set the HIP runtime shows the task only its devices and the task uses
+# the first of them.
+EXECUTOR_DEVICE_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+LOCK_DIR_VAR = "HYGEIA_DEVICE_LOCK_DIR"
+MAX_SLOTS_PER_DEVICE = 1024
+
+
+def task_device(L, n_devices: int = None, lock_dir: str = None, environ=None) -> Tuple[int, int]:
+    """The device of one `hygeia infer` task process: (device, slot).
+
+    The reference's Nextflow module starts one task process per (chrom, batch,
+    seed) (modules/two_group/4_infer.nf:28,42-48), concurrently under the local
+    executor (nextflow.config:17-21), and a task names no device. Policy:
+
+    - an executor that assigns devices (HIP_VISIBLE_DEVICES,
+      ROCR_VISIBLE_DEVICES or CUDA_VISIBLE_DEVICES set) is obeyed: the task
+      sees only those devices and takes the first (slot -1: no lock);
+    - otherwise, with more than one device, the task takes a per-node slot
+      (hyg_device_slot_acquire: an exclusive flock in $HYGEIA_DEVICE_LOCK_DIR,
+      default the temp directory, which concurrent tasks must share -- mount one
+      host directory into every task container), the first free one in the
+      order slot 0 of every device, slot 1 of every device, ...: N concurrent
+      tasks spread N / n_devices per device, and a task that ends (or dies)
+      frees its slot for the next;
+    - with one device (or none), device 0.
+
+    n_devices / lock_dir / environ default to the live values; tests pass a fake
+    device count. Selecting the device (hyg_set_device) is the caller's."""
+    import ctypes as C
+    import tempfile
+
+    env = os.environ if environ is None else environ
+    if any(env.get(v, "").strip() for v in EXECUTOR_DEVICE_VARS):
+        return 0, -1
+    n = int(L.hyg_device_count()) if n_devices is None else int(n_devices)
+    if n <= 1:
+        return 0, -1
+    d = lock_dir or env.get(LOCK_DIR_VAR) or tempfile.gettempdir()
+    dev, slot = C.c_int32(-1), C.c_int32(-1)
+    rc = L.hyg_device_slot_acquire(d.encode(), n, MAX_SLOTS_PER_DEVICE, C.byref(dev), C.byref(slot))
+    if rc != 0:  # no shared lock directory: spread by process id instead of piling onto device 0
+        return os.getpid() % n, -1
+    return int(dev.value), int(slot.value)

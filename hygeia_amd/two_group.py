@@ -150,6 +150,13 @@ def run_chains_host(observations: Dict[str, np.ndarray], n_total_reads: Dict[str
     T = tc.shape[0]
     if mc.shape != tc.shape or mk.shape != tk.shape or tk.shape[0] != T:
         raise ValueError("inconsistent count shapes")
+    if not chains:
+        raise ValueError("no chains to run")
+    n_rows = int(n_out_rows)
+    spans = sorted((int(c[4]), int(c[4]) + int(c[1])) for c in chains)
+    if spans[0][0] < 0 or spans[-1][1] > n_rows or any(a[1] > b[0] for a, b in zip(spans, spans[1:])):
+        raise ValueError("chains' output rows [out_begin, out_begin + n_sites) must be disjoint and inside "
+                         f"[0, {n_rows})")
     if max(int(c[1]) for c in chains) > model.max_duration:
         raise ValueError(f"a chain exceeds the model's max_duration {model.max_duration}")
     arr = (_lib.TgChain * len(chains))()

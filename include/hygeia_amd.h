@@ -409,6 +409,29 @@ int hyg_pre_collapse(const int64_t* cpg_pos0, int64_t n_sites, const int64_t* pl
 
 /* Number of visible HIP devices (0 when none: compute calls then fail). */
 int hyg_device_count(void);
+
+/* Device policy of concurrent task processes. The reference runs one CPU
+ * process per (chrom, batch, seed) task (modules/two_group/4_infer.nf:28,42-48),
+ * all at once under Nextflow's local executor (nextflow.config:17-21), and a
+ * task never names a device; without a policy every task of an 8-GPU node
+ * would land on device 0.
+ *
+ * hyg_device_slot_acquire takes the first free slot in the order
+ * (slot 0 of device 0, 1, ..., n_devices - 1, slot 1 of device 0, ...), a slot
+ * being an exclusive flock(2) on `<lock_dir>/hygeia_amd.gpu<d>.slot<j>.lock`
+ * held until hyg_device_slot_release or the process exits (a crashed task
+ * frees its slot), so concurrent tasks spread evenly over the devices: 16
+ * tasks on 8 devices hold two slots each. No HIP call (n_devices is the
+ * caller's: tests fake it). HYG_EINVAL when lock_dir is not usable or all
+ * max_per_device slots of every device are held; one slot per process (a
+ * second call returns the held one). hyg_set_device makes `device` the
+ * calling thread's current HIP device (hipSetDevice): models created and
+ * chains launched after it use that device. */
+int hyg_device_slot_acquire(const char* lock_dir, int32_t n_devices, int32_t max_per_device, int32_t* device,
+                            int32_t* slot);
+int hyg_device_slot_release(void);
+int hyg_set_device(int32_t device);
+int hyg_get_device(void);
 const char* hyg_last_error(void);
 const char* hyg_version(void);
 

@@ -2,7 +2,11 @@
 the CPU oracle, every output array compared):
 
 - C5 (configs[4]): 50 + 50 samples, K = 12, M = 50, B = 25 -- the emission on
-  50-sample rows (hyg_tg_emission on the device) and a whole chain;
+  50-sample rows (hyg_tg_emission on the device) and a whole chain; round 5:
+  two full-length 110 000-site chains of that shape through the production
+  (512 / 768-thread, shape-specialised) kernels, against the oracle's digests
+  (tests/golden/c5_chain_digest.json, made by tests/golden/make_c5_chain.py:
+  the oracle needs about 6 minutes per chain at this shape);
 - C3 (configs[2]): full-length segment chains of 110 000 sites (the reference's
   100 000-site segment + 2 x 5 000 buffers, run_inference_two_groups.py:67-72,
   194-218), 4 + 4 samples, K = 6, M = 50, B = 25: one on the synthetic
@@ -162,6 +166,57 @@ def test_c3_full_length_chain(oracle, long_refs, name):
     if name == "one_regime":
         dur = ref["control"][:, :, 0].astype(np.int64)
         assert dur.min() < 0  # the int16 duration output wrapped (sojourn > 32767 sites)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name", ["synthetic", "one_regime"])
+def test_c5_full_length_chain(name):
+    """C5 at full segment length: 110 000 sites, 50 + 50 samples, K = 12, M = 50,
+    B = 25, every output array bit-exact against the oracle (as digests, with
+    per-10 000-row block digests to locate a difference); one chain on the
+    synthetic model, one on a single-level stretch past the float32 hazard
+    saturation whose int16 duration outputs wrap."""
+    import importlib.util
+    import json
+    import os
+
+    from hygeia_amd import _lib
+    from hygeia_amd import synthetic as syn
+    from hygeia_amd import two_group
+
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    spec = importlib.util.spec_from_file_location("make_c5_chain", os.path.join(here, "make_c5_chain.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    with open(g.OUT) as f:
+        doc = json.load(f)
+    ref = doc["chains"][name]
+    d = g.inputs(name)
+    assert g.input_digest(d) == ref["inputs"], "the input generator changed: regenerate the fixture"
+    K, M, B, T = doc["K"], doc["M"], doc["B"], doc["T"]
+    mu, sg = syn.regime_params(K)
+    model = _model(mu, sg, two_group.uniform_theta(K, 0.8), M, B,
+                   int(max(d["tot_control"].max(), d["tot_case"].max())), T)
+    L = _lib.load()
+    # the production shape: one chain per CU at most, so the wide (512-thread
+    # forward / 768-thread backward) shape-specialised kernels run
+    assert L.hyg_tg_threads_per_chain(model.handle, 1) == 512
+    res, fw, ex = two_group.run({"control": d["meth_control"], "case": d["meth_case"]},
+                                {"control": d["tot_control"], "case": d["tot_case"]}, model, ref["seed"],
+                                ref["chain_id"])
+    out = {"merged": res.particle["merged_state"], "control": res.particle["control_state"],
+           "case": res.particle["case_state"], "split_probs": ex["split_probs"],
+           "regime_probs": ex["regime_probs"], "final_log_weights": fw, "log_z": ex["log_z"]}
+    got = g.output_record(out)
+    print(f"C5 {name}: oracle step modes {ref['modes']}, min duration output {ref['min_duration_output']}")
+    for k in g.OUTPUTS:
+        if got[k] != ref[k]:
+            blocks = [i for i, (a, b) in enumerate(zip(got.get(k + "_blocks", []), ref.get(k + "_blocks", [])))
+                      if a != b]
+            pytest.fail(f"{name}: {k} differs from the oracle (first differing {g.BLOCK}-row blocks: {blocks[:5]})")
+    assert got["log_z"] == ref["log_z"]
+    if name == "one_regime":
+        assert ref["min_duration_output"] < 0  # the int16 duration output wrapped (sojourn > 32767 sites)
 
 
 def _sg_host_chain(psg, meth, tot, seed, chain_id):

@@ -10,7 +10,8 @@ Each configuration runs many seeds as chains of ONE batched launch
     finite-state resampling active) the seed average of Z_hat / Z stays 1
     within its standard error. Cases at u = 2, the pipeline's u = 3, and u = 4,
     and (round 4) at the pipeline's K = 6 and K = 4 with 2 + 2 samples, where
-    the case transition's uniform normalisers are 1/5 and 1/4.
+    the case transition's uniform normalisers are 1/5 and 1/4, and (round 5) at
+    the stress shape's K = 12 (1/11 and 1/10).
 """
 import math
 import os
@@ -102,7 +103,7 @@ def test_resampling_gpu_vs_oracle_and_unbiased_z(oracle, K, T, M, dseed, u):
     for i, s in enumerate(seeds):
         r_ph = phantom_regime(oracle, s, cid, K)
         if r_ph not in zex:
-            zex[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+            zex[r_ph] = ex.log_z(E_ex, r_ph)
         ratios.append(math.exp(lz[i] - zex[r_ph]))
     r = np.array(ratios)
     se = r.std() / math.sqrt(len(r))
@@ -127,13 +128,14 @@ def test_backward_gpu_draws_follow_exact_smoother(oracle, K, T, dseed, u):
 
 # ----------------------------------------------------- the pipeline's K (4, 6)
 from test_tg_exact import (PIPELINE_BACKWARD, PIPELINE_KEEP_ALL, PIPELINE_RESAMPLING,  # noqa: E402
-                           draws_branch_counts)
+                           backward_seeds, draws_branch_counts)
 
 
 @pytest.mark.parametrize("K,T,dseed,u,S,M", [c[:6] for c in PIPELINE_KEEP_ALL if c[6]])
 def test_pipeline_k_keep_all_gpu_vs_oracle_and_exact(oracle, K, T, dseed, u, S, M):
-    """K = 6 / K = 4, u = 3, 2 + 2 samples, every finite particle kept: the GPU's
-    log Z is the exact log marginal likelihood (1e-12), bit for bit the oracle."""
+    """K = 6 / K = 4 / K = 12, u = 3, 2 + 2 samples, every finite particle kept:
+    the GPU's log Z is the exact log marginal likelihood (1e-12), bit for bit
+    the oracle."""
     B = 8
     p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=B, u=u, S=S)
     seeds = list(range(24))
@@ -164,7 +166,7 @@ def test_pipeline_k_resampling_gpu_unbiased_z(oracle, K, T, M, dseed, u, S):
     for i, s in enumerate(seeds):
         r_ph = phantom_regime(oracle, s, cid, K)
         if r_ph not in zex:
-            zex[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+            zex[r_ph] = ex.log_z(E_ex, r_ph)
         ratios.append(math.exp(lz[i] - zex[r_ph]))
     r = np.array(ratios)
     se = r.std() / math.sqrt(len(r))
@@ -174,7 +176,7 @@ def test_pipeline_k_resampling_gpu_unbiased_z(oracle, K, T, M, dseed, u, S):
 
 @pytest.mark.parametrize("K,T,dseed,u,S,M", [c[:6] for c in PIPELINE_BACKWARD if c[6]])
 def test_pipeline_k_backward_gpu_draws_follow_exact_smoother(oracle, K, T, dseed, u, S, M):
-    B, nseeds, cid = 60, 300, 7
+    B, nseeds, cid = 60, backward_seeds(K), 7
     p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=B, cov=2, u=u, S=S)
     seeds = list(range(nseeds))
     dc = _run_seeds(p, E, K, M, B, seeds, cid)

@@ -224,11 +224,27 @@ def test_resampling_keeps_z_unbiased(oracle, K, T, M, dseed, u):
 # is a CPU (oracle) case only; the GPU runs K = 6 up to T = 4 and K = 4 up to
 # T = 6 in the keep-all regime, and K = 6, T = 7 with resampling.
 # (K, T, data seed, u, samples per group, M, gpu)
+#
+# Round 5 adds the stress shape K = 12 (BASELINE.json configs[4]): branch 2 and
+# branch 3 draw over K - 1 = 11 regimes, a branch-4 change over K - 2 = 10.
+# K = 12 has 11, 11, 11, 1584, 6908 finite paths at t = 0..4 (397 and 1047
+# distinct states at t = 3, 4), so M = 16 keeps every path up to T = 4 (a GPU
+# case: N = 168 M candidates fit the kernel's LDS up to M of about 58) and
+# M = 1600 up to T = 5 (CPU only).
 PIPELINE_KEEP_ALL = [(6, 4, 71, 3, 2, 64, True), (4, 5, 72, 3, 2, 64, True), (4, 6, 73, 3, 2, 160, True),
-                     (6, 5, 74, 3, 2, 192, False)]
-PIPELINE_BACKWARD = [(6, 4, 81, 3, 2, 64, True), (4, 5, 82, 3, 2, 64, True), (6, 5, 83, 3, 2, 192, False)]
+                     (6, 5, 74, 3, 2, 192, False), (12, 4, 101, 3, 2, 16, True), (12, 5, 102, 3, 2, 1600, False)]
+PIPELINE_BACKWARD = [(6, 4, 81, 3, 2, 64, True), (4, 5, 82, 3, 2, 64, True), (6, 5, 83, 3, 2, 192, False),
+                     (12, 4, 111, 3, 2, 16, True)]
 # (K, T, M, data seed, u, samples per group): optimal finite-state resampling active
-PIPELINE_RESAMPLING = [(6, 7, 4, 91, 3, 2), (6, 6, 10, 92, 3, 2), (4, 8, 6, 93, 3, 2)]
+PIPELINE_RESAMPLING = [(6, 7, 4, 91, 3, 2), (6, 6, 10, 92, 3, 2), (4, 8, 6, 93, 3, 2),
+                       (12, 5, 4, 121, 3, 2), (12, 5, 8, 122, 3, 2)]
+
+
+def backward_seeds(K: int) -> int:
+    """Seeds of the backward chi-square cases: at K = 12 a branch-4 change is
+    rare enough (~1e-4 of the draws at T = 4) that 300 seeds x 60 draws would
+    show it about once; 1000 show it a few times."""
+    return 1000 if K == 12 else 300
 
 
 def branch_mass(ex, pair):
@@ -244,13 +260,14 @@ def branch_mass(ex, pair):
     return out
 
 
-def test_pipeline_k_visits_every_case_branch(oracle):
-    """The K = 6 cases exercise the case transition's K-dependent normalisers:
-    the exact smoother puts mass on branch 2 (1/(K-1) = 1/5), branch 3 (1/5) and
-    a branch-4 change (1/(K-2) = 1/4), and replacing any of those normalisers by
-    its neighbour moves the exact log Z by far more than the 1e-12 the keep-all
-    tests allow -- so those tests pin them."""
-    for K, T, dseed, u, S, M, _ in [c for c in PIPELINE_KEEP_ALL if c[0] == 6]:
+@pytest.mark.parametrize("K", [6, 12])
+def test_pipeline_k_visits_every_case_branch(oracle, K):
+    """The K = 6 and K = 12 cases exercise the case transition's K-dependent
+    normalisers: the exact smoother puts mass on branch 2 (1/(K-1): 1/5, 1/11),
+    branch 3 (1/(K-1)) and a branch-4 change (1/(K-2): 1/4, 1/10), and replacing
+    any of those normalisers by its neighbour moves the exact log Z by far more
+    than the 1e-12 the keep-all tests allow -- so those tests pin them."""
+    for K, T, dseed, u, S, M, _ in [c for c in PIPELINE_KEEP_ALL if c[0] == K]:
         p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=4, u=u, S=S)
         r_ph = phantom_regime(oracle, 0, 40, K)
         log_z, _, _, pair = ex.forward_backward(E_ex, r_ph)
@@ -304,7 +321,7 @@ def draws_branch_counts(ex, paths):
 
 @pytest.mark.parametrize("K,T,dseed,u,S,M,gpu", PIPELINE_BACKWARD)
 def test_pipeline_k_backward_draws_follow_exact_smoother(oracle, K, T, dseed, u, S, M, gpu):
-    B, nseeds = 60, 300
+    B, nseeds = 60, backward_seeds(K)
     p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=B, cov=2, u=u, S=S)
     outs = {}
 
@@ -326,7 +343,7 @@ def test_pipeline_k_backward_draws_follow_exact_smoother(oracle, K, T, dseed, u,
 
 @pytest.mark.parametrize("K,T,M,dseed,u,S", PIPELINE_RESAMPLING)
 def test_pipeline_k_resampling_keeps_z_unbiased(oracle, K, T, M, dseed, u, S):
-    nseeds = 12000
+    nseeds = 6000 if K == 12 else 12000  # K = 12: the GPU test runs 8192 seeds of the same chains
     p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2, u=u, S=S)
     zex = {}
     ratios = []
@@ -335,7 +352,7 @@ def test_pipeline_k_resampling_keeps_z_unbiased(oracle, K, T, M, dseed, u, S):
         cid = 3
         r_ph = phantom_regime(oracle, seed, cid, K)
         if r_ph not in zex:
-            zex[r_ph] = ex.forward_backward(E_ex, r_ph)[0]
+            zex[r_ph] = ex.log_z(E_ex, r_ph)
         out = oracle.chain(p, E, seed, cid, want_modes=True)
         assert out["status"] == 0
         modes.update((out["modes"][1:] // 65536).tolist())

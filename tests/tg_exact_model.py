@@ -71,6 +71,7 @@ class ExactModel:
         v1 = np.array([f32(math.log(split_prob)), f32(math.log(1 - split_prob))])
         self.lPm = np.array([v0 - logsumexp(v0), v1 - logsumexp(v1)])  # [m][m']
         self._rho = {}
+        self._succ = {}
 
     # ------------------------------------------------------------ pieces
     def rho(self, g, r, d):
@@ -157,6 +158,14 @@ class ExactModel:
         return 4
 
     def successors(self, x):
+        """[(y, log f(y | x))] over every y with a finite transition density
+        (memoised: the transitions do not depend on the phantom regime)."""
+        got = self._succ.get(x)
+        if got is None:
+            got = self._succ[x] = list(self._successors(x))
+        return got
+
+    def _successors(self, x):
         m, dc, rc, dk, rk = x
         for m2 in (0, 1):
             for dc2 in (1, dc + 1):
@@ -174,6 +183,20 @@ class ExactModel:
         return {(1, 1, i, 1, i): self.lPc[r_ph, i] for i in range(self.K) if self.lPc[r_ph, i] > -np.inf}
 
     # -------------------------------------------------------- recursions
+    def log_z(self, E, r_ph):
+        """The exact log marginal likelihood given the phantom regime alone (the
+        forward recursion of forward_backward, without the smoother)."""
+        K = self.K
+        lg = lambda t, x: E[t, x[2]] + E[t, K + x[4]]  # noqa: E731
+        alpha = {x: v + lg(0, x) for x, v in self.initial(r_ph).items()}
+        for t in range(1, E.shape[0]):
+            nxt = defaultdict(list)
+            for x, a in alpha.items():
+                for y, lf in self.successors(x):
+                    nxt[y].append(a + lf)
+            alpha = {y: logsumexp(v) + lg(t, y) for y, v in nxt.items()}
+        return logsumexp(list(alpha.values()))
+
     def forward_backward(self, E, r_ph):
         """Exact log Z and the filter / smoothing marginals given the phantom
         regime. Returns (log_z, alphas, smooth, pair) with alphas[t]: {x: log

@@ -14,7 +14,15 @@ then timed end to end:
 
 Prints one JSON line: sites x seeds / s for both, and the split of the
 batched run (parse, launch, writes).
-usage: python tools/bench_pipeline.py [--sites N] [--seeds 0,1] [--workdir DIR]
+
+--concurrent 1,4,8,16 (round 5) instead runs EVERY task of the chromosome as a
+fresh `hygeia infer` process, N at once (a thread pool of subprocesses), the
+way Nextflow's local executor runs the module's fan-out on a node
+(nextflow.config:17-21), and reports per N the aggregate sites x seeds / s and
+the per-task wall times; `infer_many` runs as a subprocess too, so the parent
+never holds a GPU context (the GPU box admits at most 16 processes on its card,
+which caps N there).
+usage: python tools/bench_pipeline.py [--sites N] [--seeds 0,1] [--workdir DIR] [--concurrent LIST]
 """
 from __future__ import annotations
 
@@ -58,12 +66,66 @@ def write_inputs(d: str, chrom: str, T: int, S: int = 4, K: int = 6):
         fh.write("data\n" + "\n".join(repr(float(x)) for x in theta) + "\n")
 
 
+# Runs one CLI command in a fresh process and prints its own phase split
+# (cli.LAST_TIMINGS) and device (cli.LAST_DEVICE) after '@@'.
+DRIVER = ("import json, sys, time; t0 = time.perf_counter(); from hygeia_amd import cli; t1 = time.perf_counter(); "
+          "rc = cli.main(sys.argv[1:]); t2 = time.perf_counter(); "
+          "print('@@' + json.dumps(dict(cli.LAST_TIMINGS, import_cli=t1 - t0, main=t2 - t1, rc=rc, "
+          "device=cli.LAST_DEVICE.get('device', -1), slot=cli.LAST_DEVICE.get('slot', -1))), flush=True)")
+
+
+def run_task(args, env=None) -> dict:
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "-c", DRIVER] + list(args), cwd=ROOT, capture_output=True, text=True,
+                       env=dict(os.environ if env is None else env, PYTHONPATH=ROOT))
+    t1 = time.perf_counter()
+    if r.returncode != 0:
+        raise RuntimeError(f"hygeia {' '.join(args[:5])} failed: {r.stderr[-2000:]}")
+    split = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("@@")][-1][2:])
+    return {"start": t0, "end": t1, "wall_s": t1 - t0, "split": split}
+
+
+def concurrent_sweep(wd, common, seeds, sites, n_batches, ns):
+    """Every (batch, seed) task as a fresh `hygeia infer` process, N at a time."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    units = sites * len(seeds)
+    tasks = [(b, sd) for b in range(n_batches) for sd in seeds]
+    out = []
+    for n in ns:
+        rdir = os.path.join(wd, f"conc{n}")
+
+        def one(t):
+            b, sd = t
+            r = run_task(["infer", "--batch", str(b), "--seed", str(sd), "--results_dir", rdir] + common)
+            print(f"  N={n} batch {b} seed {sd}: {r['wall_s']:.2f} s", file=sys.stderr, flush=True)  # progress
+            return r
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=n) as ex:
+            res = list(ex.map(one, tasks))
+        wall = time.perf_counter() - t0
+        walls = np.array([r["wall_s"] for r in res])
+        chains = np.array([r["split"].get("chains", 0.0) for r in res])
+        rec = {"concurrent": n, "tasks": len(tasks), "wall_s": wall, "value": units / wall,
+               "task_wall_s": {"mean": float(walls.mean()), "min": float(walls.min()), "max": float(walls.max())},
+               "task_chains_s": {"mean": float(chains.mean()), "max": float(chains.max())},
+               "devices": sorted({(r["split"]["device"], r["split"]["slot"]) for r in res})}
+        out.append(rec)
+        print(json.dumps(rec), flush=True)
+        shutil.rmtree(rdir, ignore_errors=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sites", type=int, default=2_400_000)
     ap.add_argument("--seeds", default="0,1")
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--concurrent", default="", help="comma list of N: every task as a process, N at once")
     a = ap.parse_args()
+    if a.concurrent:
+        return main_concurrent(a)
     from hygeia_amd import cli
 
     wd = a.workdir or tempfile.mkdtemp(prefix="hyg_pipe_")
@@ -111,6 +173,30 @@ def main():
                                    "extrapolated_s": t_one * tasks, "tasks_timed": one,
                                    "note": "each task a fresh process, as the Nextflow module runs it"},
             "input_write_s": t_write}
+    print(json.dumps(line), flush=True)
+    if a.workdir is None:
+        shutil.rmtree(wd, ignore_errors=True)
+
+
+def main_concurrent(a):
+    wd = a.workdir or tempfile.mkdtemp(prefix="hyg_pipe_")
+    chrom = "1"
+    t0 = time.perf_counter()
+    write_inputs(wd, chrom, a.sites)
+    print(f"inputs written in {time.perf_counter() - t0:.1f} s", flush=True)
+    common = ["--chrom", chrom, "--data_dir", os.path.join(wd, "data"), "--single_group_dir", os.path.join(wd, "sg")]
+    seeds = [int(x) for x in a.seeds.split(",")]
+    n_batches = a.sites // 100000 + 1
+    units = a.sites * len(seeds)
+    many = run_task(["infer_many", "--batches", "all", "--seeds", a.seeds, "--results_dir",
+                     os.path.join(wd, "many")] + common)
+    print(f"infer_many {many['wall_s']:.1f} s", flush=True)
+    sweep = concurrent_sweep(wd, common, seeds, a.sites, n_batches, [int(x) for x in a.concurrent.split(",")])
+    line = {"metric": "pipeline CpG sites x seeds / s (hygeia infer, gz CSV in -> result files out)",
+            "sites": a.sites, "seeds": seeds, "tasks": n_batches * len(seeds),
+            "infer_many": {"value": units / many["wall_s"], "wall_s": many["wall_s"], "split_s": many["split"]},
+            "concurrent_tasks": sweep,
+            "note": "each task a fresh `hygeia infer` process, N at once on one GPU (Nextflow local executor)"}
     print(json.dumps(line), flush=True)
     if a.workdir is None:
         shutil.rmtree(wd, ignore_errors=True)
