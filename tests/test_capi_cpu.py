@@ -210,3 +210,35 @@ def test_sg_compute_refuses_without_device(lib):
         assert lib.hyg_sg_emission(m, ptr(z), ptr(z), 2, T, ptr(out), None) == _lib.HYG_EDEVICE
     finally:
         lib.hyg_sg_model_destroy(m)
+
+
+def test_run_chains_host_rejects_empty_and_overlapping_chains(lib):
+    """run_chains_host refuses an empty chain list and chains whose output rows
+    [out_begin, out_begin + n_sites) overlap or leave [0, n_out_rows): the
+    kernels would write the same rows from two workgroups."""
+    from hygeia_amd import two_group
+
+    mu = [0.95, 0.05, 0.8, 0.2, 0.5, 0.5]
+    sg = [0.05, 0.05, 0.1, 0.1, 0.1, 0.2886751]
+    model = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(6, 0.8), max_total_reads=50, max_duration=100)
+    z = np.zeros((60, 2), np.uint16)
+    obs, tot = {"control": z, "case": z}, {"control": z, "case": z}
+    with pytest.raises(ValueError, match="no chains"):
+        two_group.run_chains_host(obs, tot, model, [], 10)
+    for chains, rows in (([(0, 30, 0, 1, 0), (10, 30, 1, 1, 29)], 60), ([(0, 30, 0, 1, 31)], 60),
+                         ([(0, 30, 0, 1, -1)], 60)):
+        with pytest.raises(ValueError, match="disjoint"):
+            two_group.run_chains_host(obs, tot, model, chains, rows)
+
+
+def test_threads_per_chain_m_above_64_takes_256(lib):
+    """A model with M > 64 runs the 256-thread kernels whatever its LDS (the wider
+    kernels hold one ancestor per lane); this branch needs no device."""
+    from hygeia_amd import two_group
+
+    mu = [(i + 0.5) / 12 for i in range(12)]
+    sg = [0.08 + 0.04 * (i % 2) for i in range(12)]
+    model = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(12, 0.8), num_resampled_ancestors=65,
+                                       max_total_reads=50, max_duration=100)
+    assert lib.hyg_tg_threads_per_chain(model.handle, 1) == 256
+    assert lib.hyg_tg_threads_per_chain(model.handle, 10000) == 256

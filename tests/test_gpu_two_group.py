@@ -232,8 +232,11 @@ def test_batched_host_entry(oracle):
             np.testing.assert_array_equal(r[k][o0:o0 + n], ref[rk])
         assert r["log_z"][i] == ref["log_z"]
         np.testing.assert_array_equal(r["final_w"][i], ref["final_log_weights"])
-    for bad in ([(2500, 600, 0, 1, 0)], [(0, 100, 0, 1, out)]):  # past the sites / past the output rows
-        with pytest.raises(_lib.HygError):
+    # past the sites (the C entry refuses it) / past the output rows (refused by
+    # run_chains_host's own range check, before the C entry, as overlapping rows are)
+    for bad, err in (([(2500, 600, 0, 1, 0)], _lib.HygError), ([(0, 100, 0, 1, out)], ValueError),
+                     ([(0, 100, 0, 1, 0), (0, 100, 1, 1, 50)], ValueError)):
+        with pytest.raises(err):
             two_group.run_chains_host(obs, tot, model, bad, out)
     m2 = {k: v.copy() for k, v in obs.items()}
     m2["case"][5, 0] = tot["case"][5, 0] + 1

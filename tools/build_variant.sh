@@ -10,3 +10,5 @@ for s in capi.cpp tg_kernels.hip sg_kernels.hip dmp_kernels.hip bed_kernels.hip 
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libhygeia_amd.so $D/*.o && rm -f $D/*.o && echo $D/libhygeia_amd.so
+# the sources it was built from (tools/gpu_final.sh refuses a stale variant)
+python3 -c "from hygeia_amd import build; print(build.source_hash())" > $D/source_hash

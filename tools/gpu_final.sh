@@ -29,7 +29,11 @@ step bench_c4 600 python bench.py --job c4 --steps 1 --warmup 1 --no-cpu-baselin
 step bench_c5 600 python bench.py --job c5 --steps 1 --warmup 1 --no-cpu-baseline
 step bench_c3_shard0of8 300 python bench.py --shard 0/8 --no-cpu-baseline --steps 2
 step bench_c4_shard0of8 300 python bench.py --job c4 --shard 0/8 --no-cpu-baseline --steps 1
-if [ -f $TUNE ]; then
+# the tuning build must be of the benched sources (bash tools/build_variant.sh tuning -DHYG_TUNING)
+SRC=$(python3 -c "from hygeia_amd import build; print(build.source_hash())")
+if [ -f $TUNE ] && [ "$(cat $(dirname $TUNE)/source_hash 2>/dev/null)" != "$SRC" ]; then
+  echo "[phases] the tuning library is not built from these sources ($SRC): skipped"
+elif [ -f $TUNE ]; then
   step phases_c3_shard0of8 300 env HYG_LIB_PATH=$TUNE HYG_DEBUG_PHASES=1 python bench.py --shard 0/8 --no-cpu-baseline --steps 1 --warmup 0
 fi
 step bench_c2 600 python tools/bench_sg.py
