@@ -399,7 +399,8 @@ static size_t header_bytes(int32_t n_chains) {
 
 size_t hyg_tg_workspace_bytes(const hyg_tg_model* m, int32_t n_chains, int64_t total_steps) {
   if (!m || n_chains < 0 || total_steps < 0) return 0;
-  return header_bytes(n_chains) + (size_t)total_steps * record_bytes(m->c.M) + 256;
+  return header_bytes(n_chains) + (size_t)total_steps * record_bytes(m->c.M) + 256 +
+         (size_t)n_chains * backward_scratch_bytes(m->c);
 }
 
 int hyg_tg_run_chains(const hyg_tg_model* m, const hyg_tg_chain* chains, int32_t n_chains, const double* E,
@@ -428,6 +429,13 @@ int hyg_tg_run_chains(const hyg_tg_model* m, const hyg_tg_chain* chains, int32_t
     cd[i].T = c.n_sites;
     cd[i].pad = 0;
     off += (size_t)c.n_sites * rb;
+  }
+  // the backward's full-N weight scratch of each chain (backward_global_w), behind the records
+  const size_t sb = backward_scratch_bytes(m->c);
+  off = (off + 255) / 256 * 256;
+  for (int i = 0; i < n_chains; ++i) {
+    cd[i].wg_offset = sb ? (int64_t)off : 0;
+    off += sb;
   }
   if (off > workspace_bytes) return fail(HYG_EINVAL, "workspace too small (see hyg_tg_workspace_bytes)");
   uint8_t* ws = (uint8_t*)workspace;

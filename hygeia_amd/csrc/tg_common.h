@@ -28,6 +28,7 @@ struct ChainDev {
   uint64_t chain_id;
   int32_t T;
   int32_t pad;
+  int64_t wg_offset;  // byte offset of the backward's full-N weight scratch (Nmax f64; backward_global_w)
 };
 
 // Per-step history record: scalars, then M packed parent states, then M
@@ -80,5 +81,13 @@ int tg_threads_per_chain(const hyg_tg_consts& c, int n_chains);  // forward work
 int tg_force_threads(int fwd, int bwd);                           // test override (0 = automatic)
 int tg_resident_per_cu(const hyg_tg_consts& c, int n_chains);     // forward workgroups per CU
 size_t tg_layout_bytes(const hyg_tg_consts& c, int threads, bool backward);  // LDS of one chain (0: bad width)
+// Whether a model's backward keeps its full-N weights (the general path and the
+// final step's draw) in a per-chain global scratch of Nmax f64 instead of LDS,
+// so that its LDS holds several chains per CU (the C5 shape); the workspace
+// then carries n_chains * backward_scratch_bytes(c) more bytes.
+bool backward_global_w(const hyg_tg_consts& c);
+inline size_t backward_scratch_bytes(const hyg_tg_consts& c) {
+  return backward_global_w(c) ? ((size_t)c.Nmax * sizeof(double) + 255) / 256 * 256 : 0;
+}
 
 }  // namespace hyg

@@ -347,16 +347,26 @@ struct Lay {  // byte offsets into the dynamic LDS (32-bit: one SGPR each in the
   uint32_t bcnt_bytes;
   int npad, nkeys, nt;
   int topset_r;  // keys per lane of the top-set sort: A holds <= 64 * topset_r per wave
+  int lcap;      // backward: doubles of the list / logit area at W (Nmax, or the lists alone with gw)
 };
 
-__host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT, bool backward) {
+// The backward's list area without the full-N weights (gw): the segment lists
+// (16 slots x 64 logits, then 64 u128 masses and 64 indices), or an appended
+// list of up to 4 (NT + 1) logits (its indices in the cp area), or 64 logits
+// and their masses: doubles.
+__host__ __device__ constexpr int bwd_list_doubles(int NT) {
+  return (64 * 16 + 128 + 32) > 4 * (NT + 1) ? (64 * 16 + 128 + 32) : 4 * (NT + 1);
+}
+
+__host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT, bool backward, bool gw = false) {
   // Sized for 3 workgroups per CU at K = 6, M = 50, NT = 256 (<= 53 KiB each).
   Lay l{};
   l.nt = NT;
   l.topset_r = 1;
   l.npad = Nmax;
+  l.lcap = (backward && gw && bwd_list_doubles(NT) < Nmax) ? bwd_list_doubles(NT) : Nmax;
   size_t o = 0;
-  l.W = o; o = align_up(o + sizeof(double) * l.npad, 16);
+  l.W = o; o = align_up(o + sizeof(double) * (backward ? l.lcap : l.npad), 16);
   if (backward) {
     // the backward's list / logit area is the weight area: the list path
     // builds no weights and the general path turns the weights into logits
@@ -2104,24 +2114,38 @@ __device__ __forceinline__ void backward_bits(uint64_t* rb, int B, int t, uint64
   }
 }
 
-template <int NT, int KC = 0, int MC = 0, int BC = 0, bool PHS = false>  // KC > 0: one model shape (see tg_forward_kernel)
+// GW: the full-N weights (the final step's draw and the general path) live in
+// the chain's global scratch (ChainDev::wg_offset of `wscr`, the same workspace
+// as `ws`, disjoint bytes) instead of LDS, whose W area then holds the lists
+// alone (make_layout gw): several chains per CU at the C5 shape. Global W is
+// handed between threads behind __syncthreads (its vmcnt(0) release), only on
+// the steps that build it.
+template <int NT, int KC = 0, int MC = 0, int BC = 0, bool PHS = false, bool GW = false>  // KC > 0: one model shape (see tg_forward_kernel)
 __global__ void __launch_bounds__(NT, (NT == 512 ? 1 : 3))
 tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double* __restrict__ E,
                    const uint8_t* __restrict__ ws, const int32_t* status_in, int16_t* __restrict__ o_merged,
                    int16_t* __restrict__ o_control, int16_t* __restrict__ o_case, float* __restrict__ o_split,
                    float* __restrict__ o_regime, int32_t* status_out, Lay lay_arg,
-                   unsigned long long* __restrict__ dbg_arg) {
+                   unsigned long long* __restrict__ dbg_arg, uint8_t* __restrict__ wscr) {
   unsigned long long* __restrict__ const dbg = PHS ? dbg_arg : nullptr;  // (see tg_forward_kernel)
   const hyg_tg_consts* __restrict__ c = md.consts;
   const int K = KC ? KC : c->K, M = KC ? MC : c->M, B = KC ? BC : c->B, I = KC ? 2 * KC + KC * KC : c->I,
             K2 = 2 * K, tid = threadIdx.x;
-  const int Nmax = KC ? MC * (2 * KC + KC * KC) : c->Nmax;  // hoisted: see sig_thresh in tg_forward_kernel
-  const Lay lay = KC ? make_layout(KC, MC, BC, MC * (2 * KC + KC * KC), NT, true) : lay_arg;
+  const Lay lay = KC ? make_layout(KC, MC, BC, MC * (2 * KC + KC * KC), NT, true, GW) : lay_arg;
+  const int Lcap = lay.lcap;  // doubles of the list area (Nmax without GW)
   const ChainDev ch = chains[blockIdx.x];
   const int T = ch.T;
   if (status_in[blockIdx.x] != HYG_OK) return;  // uniform
   extern __shared__ __align__(16) unsigned char smem[];
-  double* W = (double*)(smem + lay.W);
+  double* W;
+  if constexpr (GW) W = (double*)(wscr + ch.wg_offset);
+  else W = (double*)(smem + lay.W);
+  // a barrier behind which every thread's W writes are visible (LDS: the
+  // LDS-only barrier; global W: a workgroup release of the stores)
+  auto w_barrier = [&]() {
+    if constexpr (GW) __syncthreads();
+    else lds_barrier();
+  };
   double* Lg = (double*)(smem + lay.L);
   uint64_t* pst = (uint64_t*)(smem + lay.pst);
   double* pw = (double*)(smem + lay.pw);
@@ -2246,7 +2270,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
     // The rows of the backward kernel need the weights of the few candidates
     // that can reach a trajectory's next state only (the list path); all N
     // weights are built for the final step's draw and for the general path.
-    const bool fast = (s.mode != MODE_INIT) && np <= 64 && B <= 64 && Nmax >= 192 && t != T - 1;
+    const bool fast = (s.mode != MODE_INIT) && np <= 64 && B <= 64 && Lcap >= 192 && t != T - 1;
     bool w_ready = false;
     auto make_W = [&]() {
       if (s.mode == MODE_INIT) gen_weights_init<NT>(cl, K, s.r_ph, Et, W, &mloc, &cloc);
@@ -2293,7 +2317,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
         ebuf[q] = (i < e_tot) ? Ech[(size_t)t0 * K2 + i] : 0.0;
       }
     }
-    if (!fast) lds_barrier();  // W written by every thread (the list path reads only LDS written behind barriers)
+    if (!fast) w_barrier();  // W written by every thread (the list path reads only LDS written behind barriers)
     BPH(1);
     auto state_of = [&](int n) -> uint64_t {
       if (s.mode == MODE_INIT) return init_state(K, n);
@@ -2388,12 +2412,12 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
           // Segment list (at most kSeg reachable slots): slot v's finite logits
           // at [64 v, 64 v + c_v) in lane order, so the list is in n order by
           // construction: no shared counter, no atomics, no rank sort
-          segp = nseg <= kSeg && Nmax >= 64 * kSeg + 160 && 4 * (NT + 1) >= 64 * kSeg;
+          segp = nseg <= kSeg && Lcap >= 64 * kSeg + 160 && 4 * (NT + 1) >= 64 * kSeg;
           if (!segp) {
             if (tid == 0) sh.cnt = 0;
             lds_barrier();  // (the segment path: every reader of the areas is behind the last group's barrier)
           }
-          const int cap = (4 * (NT + 1) < Nmax) ? 4 * (NT + 1) : Nmax;
+          const int cap = (4 * (NT + 1) < Lcap) ? 4 * (NT + 1) : Lcap;
           constexpr int NW = NT / 64;
           const int lane = lane_id(), wv = wave_id();
           const bool act = lane < np;
@@ -2469,7 +2493,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
           L = segp ? __builtin_amdgcn_readlane(seg_incl, 63) : sh.cnt;
           if (dbg && tid == 0) ph_acc[11] += L;
           if (L == 0) { fail = true; break; }  // uniform: every logit -inf
-          one_wave = L <= 64 && Nmax >= 192;
+          one_wave = L <= 64 && Lcap >= 192;
         }
         if (pre_bits && g == 0 && t >= 1 && wave_id() == NT / 64 - 1)  // next step's bits, while wave 0 draws
           backward_bits(rb + ((t - 1) & 1) * rbs, B, t - 1, ch.seed, ch.chain_id);
@@ -2553,9 +2577,9 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             pend = -1;
           }
           if (!w_ready) {
-            lds_barrier();  // the list areas (= the W area) are reused below
+            w_barrier();  // the list areas (= the W area) are reused below
             make_W();
-            lds_barrier();
+            w_barrier();
           }
           double m = HYG_NINF;
           for (int n = tid; n < N; n += NT) {
@@ -2568,6 +2592,7 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
             W[n] = l;  // each n read and rewritten by one thread
             m = dmax(m, l);
           }
+          if constexpr (GW) __syncthreads();  // the categorical reads other threads' logits
           w_ready = false;  // W holds this group's logits now
           const double lmax = block_max<NT>(m, red);
           if (!(lmax > HYG_NINF)) { fail = true; break; }  // uniform: every logit -inf
@@ -2751,7 +2776,10 @@ int threads_per_chain(bool backward, const hyg_tg_consts& c, int n_chains) {
   if (c.M > 64) return def;  // the wider kernels assume the pipeline's M <= 64 (one ancestor per lane)
   const size_t lds = make_layout(c.K, c.M, c.B, c.Nmax, def, false).total;
   // (C5: the backward's list path keeps its 12 waves busy: 768 threads, 6 %
-  // faster than 512 in r03d; the forward is faster at 512)
+  // faster than 512 in r03d; the forward is faster at 512). With more chains
+  // than CUs the C5 backward runs at 256 threads with its full-N weights in
+  // global memory (GW): three chains per CU instead of one.
+  if (backward && backward_global_w(c) && n_chains > device_cus()) return 256;
   if (2 * lds > 160 * 1024) return backward ? 768 : 512;
   if (n_chains <= device_cus()) return lowocc ? lowocc : (backward ? kLowOccThreadsBwd : kLowOccThreads);
   return def;
@@ -2783,11 +2811,15 @@ int last_kernel_ms(float* out3) {
 size_t forward_lds_bytes(const hyg_tg_consts& c, int n_chains) {
   return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(false, c, n_chains), false).total;
 }
+static bool bwd_gw(const hyg_tg_consts& c, int NT);
 size_t tg_layout_bytes(const hyg_tg_consts& c, int threads, bool backward) {
-  return valid_width(threads) ? make_layout(c.K, c.M, c.B, c.Nmax, threads, backward).total : 0;
+  return valid_width(threads)
+             ? make_layout(c.K, c.M, c.B, c.Nmax, threads, backward, backward && bwd_gw(c, threads)).total
+             : 0;
 }
 size_t backward_lds_bytes(const hyg_tg_consts& c, int n_chains) {
-  return make_layout(c.K, c.M, c.B, c.Nmax, threads_per_chain(true, c, n_chains), true).total;
+  const int nt = threads_per_chain(true, c, n_chains);
+  return make_layout(c.K, c.M, c.B, c.Nmax, nt, true, bwd_gw(c, nt)).total;
 }
 
 int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* meth_c, const uint16_t* tot_c,
@@ -2813,11 +2845,16 @@ static bool shape_specialised(const hyg_tg_consts& c) {
   static const bool off = tuning_env("HYG_NO_SHAPE") != nullptr;
   return !off && c.K == 6 && c.M == 50 && c.B == 25 && c.I == 48 && c.Nmax == 2400;
 }
-// the stress shape (C5: K = 12, M = 50, B = 25), one chain per CU at 512 threads
+// the stress shape (C5: K = 12, M = 50, B = 25): the forward one chain per CU
+// at 512 threads, the backward at 768 or, with its full-N weights in global
+// memory (GW, more chains than CUs), at 256
 static bool shape_c5(const hyg_tg_consts& c) {
   static const bool off = tuning_env("HYG_NO_SHAPE") != nullptr;
   return !off && c.K == 12 && c.M == 50 && c.B == 25 && c.I == 168 && c.Nmax == 8400;
 }
+bool backward_global_w(const hyg_tg_consts& c) { return shape_c5(c); }
+// the backward instantiation of a width keeps its full-N weights in global memory
+static bool bwd_gw(const hyg_tg_consts& c, int NT) { return NT == 256 && backward_global_w(c); }
 // HYG_DEBUG_PHASES=1 selects the phase-timer instantiations (256 and 512 threads).
 static bool want_phases() {
   static const bool on = tuning_env("HYG_DEBUG_PHASES") != nullptr;
@@ -2841,6 +2878,9 @@ FwdFn fwd_kernel(const hyg_tg_consts& c) {
 }
 template <int NT>
 BwdFn bwd_kernel(const hyg_tg_consts& c) {
+  if constexpr (NT == 256)
+    if (bwd_gw(c, NT)) return want_phases() ? &tg_backward_kernel<NT, 12, 50, 25, true, true>
+                                            : &tg_backward_kernel<NT, 12, 50, 25, false, true>;
   if constexpr (has_phases<NT>()) {
     if (want_phases()) {
       if (shape_specialised(c)) return &tg_backward_kernel<NT, 6, 50, 25, true>;
@@ -2912,7 +2952,7 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
 template <int NT>
 static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
                               const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
-  const Lay lb = make_layout(c.K, c.M, c.B, c.Nmax, NT, true);
+  const Lay lb = make_layout(c.K, c.M, c.B, c.Nmax, NT, true, bwd_gw(c, NT));
   if (lb.total > 160 * 1024) return HYG_EUNSUPPORTED;
   if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
   if (hipFuncSetAttribute((const void*)bwd_kernel<NT>(c), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2925,7 +2965,7 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
   ev_record(2, false, s);
   hipLaunchKernelGGL(bwd_kernel<NT>(c), dim3(n_chains), dim3(NT), lb.total, s, md, chains_dev, E,
                      (const uint8_t*)ws, (const int32_t*)out.status, out.merged, out.control, out.kase,
-                     out.split_probs, out.regime_probs, out.status, lb, dbgb);
+                     out.split_probs, out.regime_probs, out.status, lb, dbgb, ws);
   ev_record(2, true, s);
   if (dbgb) {
     std::vector<unsigned long long> h((size_t)kPh * n_chains);

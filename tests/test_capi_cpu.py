@@ -242,3 +242,22 @@ def test_threads_per_chain_m_above_64_takes_256(lib):
                                        max_total_reads=50, max_duration=100)
     assert lib.hyg_tg_threads_per_chain(model.handle, 1) == 256
     assert lib.hyg_tg_threads_per_chain(model.handle, 10000) == 256
+
+
+def test_c5_backward_keeps_full_weights_in_global_memory(lib):
+    """The C5 shape's 256-thread backward (GW) holds its lists alone in LDS: three
+    chains per CU fit (the LDS W of 8 400 f64 held one); its full-N weights take
+    one Nmax f64 scratch per chain in the workspace. No device needed."""
+    from hygeia_amd import synthetic as syn
+    from hygeia_amd import two_group
+
+    mu, sg = syn.regime_params(12)
+    m = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(12, 0.8), max_total_reads=300, max_duration=1000)
+    assert 3 * lib.hyg_tg_lds_bytes(m.handle, 256, 1) <= 160 * 1024
+    assert lib.hyg_tg_lds_bytes(m.handle, 768, 1) > 8400 * 8  # the one-per-CU width keeps W in LDS
+    one, two = (lib.hyg_tg_workspace_bytes(m.handle, n, 1000) for n in (1, 2))
+    assert two - one >= 8400 * 8
+    mu6, sg6 = syn.regime_params(6)
+    m6 = two_group.CaseControlModel(mu6, sg6, two_group.uniform_theta(6, 0.8), max_total_reads=300, max_duration=1000)
+    one6, two6 = (lib.hyg_tg_workspace_bytes(m6.handle, n, 1000) for n in (1, 2))
+    assert two6 - one6 < 2400 * 8  # no scratch for the pipeline shape

@@ -169,13 +169,16 @@ def test_c3_full_length_chain(oracle, long_refs, name):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("bwd", [0, 256])
 @pytest.mark.parametrize("name", ["synthetic", "one_regime"])
-def test_c5_full_length_chain(name):
+def test_c5_full_length_chain(name, bwd):
     """C5 at full segment length: 110 000 sites, 50 + 50 samples, K = 12, M = 50,
     B = 25, every output array bit-exact against the oracle (as digests, with
     per-10 000-row block digests to locate a difference); one chain on the
     synthetic model, one on a single-level stretch past the float32 hazard
-    saturation whose int16 duration outputs wrap."""
+    saturation whose int16 duration outputs wrap. bwd = 256: the backward width
+    of a C5 launch with more chains than CUs, whose full-N weights live in
+    global memory (GW); 0: the automatic width of one chain (768, LDS)."""
     import importlib.util
     import json
     import os
@@ -201,9 +204,13 @@ def test_c5_full_length_chain(name):
     # the production shape: one chain per CU at most, so the wide (512-thread
     # forward / 768-thread backward) shape-specialised kernels run
     assert L.hyg_tg_threads_per_chain(model.handle, 1) == 512
-    res, fw, ex = two_group.run({"control": d["meth_control"], "case": d["meth_case"]},
-                                {"control": d["tot_control"], "case": d["tot_case"]}, model, ref["seed"],
-                                ref["chain_id"])
+    assert L.hyg_tg_force_threads(0, bwd) == 0
+    try:
+        res, fw, ex = two_group.run({"control": d["meth_control"], "case": d["meth_case"]},
+                                    {"control": d["tot_control"], "case": d["tot_case"]}, model, ref["seed"],
+                                    ref["chain_id"])
+    finally:
+        L.hyg_tg_force_threads(0, 0)
     out = {"merged": res.particle["merged_state"], "control": res.particle["control_state"],
            "case": res.particle["case_state"], "split_probs": ex["split_probs"],
            "regime_probs": ex["regime_probs"], "final_log_weights": fw, "log_z": ex["log_z"]}
