@@ -623,6 +623,13 @@ def main(argv: Sequence[str] = None) -> int:
     if cmd == "make_bed_file":  # the single-group container's subcommand
         from . import bed
         return bed.make_bed_file_main(rest)
+    if cmd == "estimate_parameters_and_regimes":  # the single-group container's subcommand (pipeline step 2)
+        from . import single_group
+        try:
+            return single_group.main(rest)
+        except FlagError as e:
+            print(f"Error: {e}", file=sys.stderr)
+            return 1
     if cmd in ("version", "-v", "--version"):
         from . import _lib
         print("Hygeia version {} ({})".format(os.environ.get("HYGEIA_VERSION", ""),
@@ -634,7 +641,8 @@ def main(argv: Sequence[str] = None) -> int:
               "  infer     - Run inference on two groups (MI355X)\n"
               "  infer_many - Every (batch, seed) task of a chromosome in one launch (MI355X)\n"
               "  aggregate - Aggregate results\n  get_dmps  - Get DMPs (Differentially Methylated Positions)\n"
-              "  make_bed_file - Regime BED track of a single-group regimes CSV (MI355X)")
+              "  make_bed_file - Regime BED track of a single-group regimes CSV (MI355X)\n"
+              "  estimate_parameters_and_regimes - Single-group regimes and parameters (MI355X)")
         return 0
     if cmd in COMMANDS.split():
         print(f"Error: '{cmd}' is not part of the MI355X inference path; use the reference pipeline step",
