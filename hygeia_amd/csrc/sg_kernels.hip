@@ -83,6 +83,7 @@ __device__ __forceinline__ hyg_u128 sg_ceil_mul_f64(double T, hyg_u128 R) {
 
 // ------------------------------------------------------------ LDS layout
 constexpr int kSgChunk = 32;  // pending entries finalised per smoothing round
+constexpr int kSgPh = 24;     // phase-timer slots (HYG_SG_PHASES builds; the last holds the latest stamp)
 
 struct SgShared {
   int npend, nfree, cur, status;
@@ -90,7 +91,7 @@ struct SgShared {
   unsigned int lmask;  // free psi slots resident in LDS
   int pad1;
   double logC;
-  unsigned long long ph[16];  // phase timers (diagnostic runs only)
+  unsigned long long ph[kSgPh];  // phase timers (diagnostic runs only)
 };
 
 struct SgLay {
@@ -532,12 +533,12 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
   // 5 normalise, 6 smoothing, 7 compaction; counters 8 optimal steps, 9
   // keep-top steps, 10 K-loop iterations, 11 pending entries, 12 parameter
   // estimation (phi, updates, rebuilds), 15 = last stamp
-  if (tid < 16) sh.ph[tid] = 0;
+  if (tid < kSgPh) sh.ph[tid] = 0;
 #define SG_PH(k)                                                   \
   if (dbg && tid == 0) {                                           \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-    sh.ph[k] += now_ - sh.ph[15];                                  \
-    sh.ph[15] = now_;                                              \
+    sh.ph[k] += now_ - sh.ph[kSgPh - 1];                           \
+    sh.ph[kSgPh - 1] = now_;                                       \
   }
 #define SG_CNT(k, v) \
   if (dbg && tid == 0) sh.ph[k] += (v);
@@ -586,7 +587,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
   double BKr[KHr];
 #pragma unroll
   for (int j = 0; j < KHr; ++j) BKr[j] = 0.0;
-  if (dbg && tid == 0) sh.ph[15] = __builtin_amdgcn_s_memtime();
+  if (dbg && tid == 0) sh.ph[kSgPh - 1] = __builtin_amdgcn_s_memtime();
   for (int t = 0; t < T; ++t) {
     const int cb = t & 1, pb = cb ^ 1;  // LDS buffers of the current / previous particle sets
     int M = 0, Np = N;
@@ -864,6 +865,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       }
       if (tid < NT && va > HYG_NINF)
         __hip_atomic_fetch_max(Amax + vr, va, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (!PE) { SG_PH(7); }
       {
         // the continuing particles' part of the block max and finite count of
         // the new log-weights rides on this barrier; the fresh particles' part
@@ -876,6 +878,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         }
       }
       lds_barrier();
+      if (!PE) { SG_PH(16); }
       const double ea = (va > HYG_NINF) ? hyg_exp(va - Amax[vr]) : 0.0;
       if (tid < NT && va > HYG_NINF) {
         const hyg_u128 im = hyg_fix100(ea);  // < 2^101: limbs of 34, 34 and 33 bits
@@ -897,7 +900,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
           if (r == 0) mqv[q] = m;
         }
       }
+      if (!PE) { SG_PH(17); }
       lds_barrier();
+      if (!PE) { SG_PH(11); }
       if (tid < K) {
         const double m = mqv[tid];
         double S = 0.0;
@@ -916,7 +921,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         lsev[tid] = (m > HYG_NINF) ? m + hyg_log(S) : HYG_NINF;  // log-normaliser of row q
         lsev[K + tid] = (m > HYG_NINF) ? 1.0 / S : 0.0;
       }
+      if (!PE) { SG_PH(18); }
       lds_barrier();
+      if (!PE) { SG_PH(19); }
 #pragma unroll
       for (int j = 0; j < KH; ++j) {  // this thread's entries of the backward kernels (record of step t)
         const int q = q0 + j < K ? q0 + j : K - 1;
@@ -937,6 +944,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       // record t-1 (stored at the end of step t-1) is drained by every wave
       // here, before the barriers of the reductions; published after them
       sg_drain_stores();
+      if (!PE) { SG_PH(20); }
       // block max and finite count of the N new log-weights: the continuing
       // particles' wave partials and the K fresh ones (lsev[q] + log g_t(q), as
       // formed above), the same values as one block reduction (a max is exact)
@@ -963,7 +971,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         if ((NB == NT) || wv < NT / 64) fx = hyg_exp_fix100(nlw - mx);  // waves >= 4 hold no particle
         // (no leading barrier: red's last readers, the weights' partials, are
         // behind the weights' last barrier)
-        logZ = mx + hyg_log(hyg_u128_to_f64(block_sum128<NB, false>(fx, red), 100));
+        const hyg_u128 Sx = block_sum128<NB, false>(fx, red);
+        if (!PE) { SG_PH(21); }
+        logZ = mx + hyg_log(hyg_u128_to_f64(Sx, 100));
       }
       if (tid == 0) sg_st4(ctl, (unsigned)t);  // records 0 .. t-1 are published
       my_lw = nlw;
@@ -1188,8 +1198,8 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
     else sg_st4(ctl + 8, (unsigned)(-status));
   }
 
-  if (dbg && tid < 15) dbg[(size_t)chain * 16 + tid] = sh.ph[tid];
-  if (dbg && tid == 15) dbg[(size_t)chain * 16 + 15] = (unsigned long long)T;
+  if (dbg && tid < kSgPh - 1) dbg[(size_t)chain * kSgPh + tid] = sh.ph[tid];
+  if (dbg && tid == kSgPh - 1) dbg[(size_t)chain * kSgPh + kSgPh - 1] = (unsigned long long)T;
 #undef SG_PH
 #undef SG_CNT
 }
@@ -1489,7 +1499,7 @@ static void launch_chain_kt(const SgModelDev& md, const SgChainDev* chains_dev, 
   for (int c0 = 0; c0 < n_chains; c0 += per) {
     const int nc = (n_chains - c0) < per ? (n_chains - c0) : per;
     hipLaunchKernelGGL((sg_chain_kernel<KT, NB, PE, PHS>), dim3(2 * nc), dim3(NB), lds, s, md, chains_dev + c0, nc, E,
-                       ws, cap, probs, status + c0, lay, clay, dbg ? dbg + (size_t)16 * c0 : nullptr, pe);
+                       ws, cap, probs, status + c0, lay, clay, dbg ? dbg + (size_t)kSgPh * c0 : nullptr, pe);
     if ((*err = hipGetLastError()) != hipSuccess) return;
   }
 }
@@ -1522,8 +1532,8 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
   unsigned long long* dbg = nullptr;
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(ctl, 0, kSgCtlBytes * (size_t)n_chains, s) != hipSuccess) return HYG_EDEVICE;
-  if (want_dbg && hipMalloc((void**)&dbg, sizeof(unsigned long long) * 16 * n_chains) != hipSuccess) dbg = nullptr;
-  if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * 16 * n_chains, s);
+  if (want_dbg && hipMalloc((void**)&dbg, sizeof(unsigned long long) * kSgPh * n_chains) != hipSuccess) dbg = nullptr;
+  if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * kSgPh * n_chains, s);
   hipError_t err = hipErrorInvalidValue;
   switch (c.K) {
 #define SG_CASE(k)                                                                                               \
@@ -1552,37 +1562,42 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
     return HYG_EDEVICE;
   }
   if (dbg) {
-    std::vector<unsigned long long> h((size_t)16 * n_chains);
+    std::vector<unsigned long long> h((size_t)kSgPh * n_chains);
     (void)hipStreamSynchronize(s);
     (void)hipMemcpy(h.data(), dbg, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
     (void)hipFree(dbg);
     // the longest chain (the critical path)
     int lc = 0;
     for (int i = 1; i < n_chains; ++i)
-      if (h[(size_t)i * 16 + 15] > h[(size_t)lc * 16 + 15]) lc = i;
-    const double steps = (double)h[(size_t)lc * 16 + 15];
-    const char* nm[8] = {"copy", "sort", "kloop", "resample", "weights", "normalise", "record", "-"};
+      if (h[(size_t)i * kSgPh + kSgPh - 1] > h[(size_t)lc * kSgPh + kSgPh - 1]) lc = i;
+    const unsigned long long* hl = h.data() + (size_t)lc * kSgPh;
+    const double steps = (double)hl[kSgPh - 1];
+    auto v = [&](int k) { return (double)hl[k] / steps; };
     fprintf(stderr, "[hyg sg phases] K=%d lds=%zu smoothing slots_lds=%d longest chain %d: %.0f steps, cycles/step:",
             c.K, lds, clay.nl, lc, steps);
     double sum = 0;
-    for (int k = 0; k < 8; ++k) {
-      const double v = (double)h[(size_t)lc * 16 + k] / steps;
-      fprintf(stderr, " %s=%.0f", nm[k], v);
-      sum += v;
+    if (!pe) {
+      const char* nm[22] = {"copy", "sort", "kloop", "resample", "weights.tail", "normalise.tail", "record",
+                            "weights.amax", "-", "-", "-", "weights.limbsG", "bitonic", "gather+mono", "log+scan",
+                            "-", "weights.bar1", "weights.bar2", "weights.S", "weights.bar3", "normalise.drain",
+                            "normalise.sum"};
+      for (int k = 0; k < 22; ++k) {
+        if (nm[k][0] == '-') continue;
+        fprintf(stderr, " %s=%.0f", nm[k], v(k));
+        sum += v(k);
+      }
+    } else {
+      const char* nm[7] = {"copy", "sort", "kloop", "resample", "weights", "normalise", "record"};
+      for (int k = 0; k < 7; ++k) {
+        fprintf(stderr, " %s=%.0f", nm[k], v(k));
+        sum += v(k);
+      }
+      fprintf(stderr, " estimation=%.0f rebuild=%.0f (rows/rebuild %.0f)", v(12), v(13),
+              (double)hl[14] / std::max(1.0, steps / (double)pe->c.every));
+      sum += v(12) + v(13);
     }
-    const double pe_c = (double)h[(size_t)lc * 16 + 12] / steps, pe_r = (double)h[(size_t)lc * 16 + 13] / steps;
-    if (!pe)
-      fprintf(stderr, " [sort split: bitonic=%.0f gather+mono=%.0f log+scan=%.0f]", pe_c, pe_r,
-              (double)h[(size_t)lc * 16 + 14] / steps);
-    if (pe)
-      fprintf(stderr, " estimation=%.0f rebuild=%.0f (rows/rebuild %.0f)", pe_c, pe_r,
-              (double)h[(size_t)lc * 16 + 14] / std::max(1.0, steps / (double)pe->c.every));
-    if (pe) sum += pe_c + pe_r;
-    fprintf(stderr, " total=%.0f | optimal=%.0f keep_top=%.0f kloop_iters/capped=%.2f pending/step=%.2f\n", sum,
-            (double)h[(size_t)lc * 16 + 8], (double)h[(size_t)lc * 16 + 9],
-            (double)h[(size_t)lc * 16 + 10] /
-                std::max(1.0, (double)(h[(size_t)lc * 16 + 8] + h[(size_t)lc * 16 + 9])),
-            (double)h[(size_t)lc * 16 + 11] / steps);
+    fprintf(stderr, " total=%.0f | optimal=%.0f keep_top=%.0f kloop_iters/capped=%.2f\n", sum, (double)hl[8],
+            (double)hl[9], (double)hl[10] / std::max(1.0, (double)(hl[8] + hl[9])));
   }
   return HYG_OK;
 }

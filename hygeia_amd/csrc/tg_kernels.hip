@@ -330,16 +330,6 @@ constexpr int kLRof = NT >= 768 ? 2 : (NT >= 512 ? HYG_LR512 : HYG_LR256);
 #endif
 template <int NT>
 constexpr int kSortWaves = (NT / 64 < HYG_SORT_WAVES) ? NT / 64 : HYG_SORT_WAVES;
-// The top set sorted by rank counting (top_set_finish1): each sorting lane
-// counts the keys of A below its own (broadcast LDS reads, no dependent
-// compare-exchange stages) and scatters it to its rank, one barrier. At one
-// chain per CU (NT >= 512) the step's latency is what counts; at 256 threads
-// (three chains per CU, issue-bound) the bitonic's fewer instructions do.
-#ifndef HYG_RANK_SORT
-#define HYG_RANK_SORT 1
-#endif
-template <int NT>
-constexpr bool kRankSort = HYG_RANK_SORT && NT >= 512;
 
 struct Lay {  // byte offsets into the dynamic LDS (32-bit: one SGPR each in the kernels)
   uint32_t W, L, keys, bcnt, bpos, pre64, part, cp, pst, pw, phz, pf, ering, cl, parents, X, grp, gst, rb, xo, red,
@@ -1285,25 +1275,8 @@ __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB,
   hyg_u192 f = hyg_u192_zero(), inc = hyg_u192_zero();
   if (sorter) {
     e[0] = (base < nA) ? srt[base] : ~0ull;
-    if constexpr (kRankSort<NT>) {
-      // rank of this lane's key among A's nA keys (unique: the index breaks
-      // value ties), two keys per broadcast read (srt holds >= nA + 1 slots)
-      const uint64_t k = e[0];
-      int r0 = 0, r1 = 0;
-#pragma unroll 4
-      for (int j = 0; j < nA; j += 2) {  // nA is wave-uniform
-        const ulonglong2 kk = *(const ulonglong2*)(srt + j);
-        r0 += (kk.x < k) ? 1 : 0;
-        r1 += ((j + 1 < nA) & (kk.y < k)) ? 1 : 0;
-      }
-      uint64_t* sorted = (uint64_t*)scr;  // the bitonic's exchange buffers (2 x 64 NSW keys)
-      if (base < nA) sorted[r0 + r1] = k;
-      lds_barrier();
-      e[0] = (base < nA) ? sorted[base] : ~0ull;
-    } else {
-      int ib = 0;
-      Bitonic<64 * NSW, 1, 2, 1>::run(e, (uint64_t*)scr, ib);
-    }
+    int ib = 0;
+    Bitonic<64 * NSW, 1, 2, 1>::run(e, (uint64_t*)scr, ib);
     TPH(27);
     // (every wave loaded its keys before the first cross-wave barrier)
     srt[base] = e[0];
@@ -1318,7 +1291,7 @@ __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB,
     // sort's first cross-wave barrier, the second after its last (both before
     // the first barrier delay the sort: measured)
     static_assert(!SPLIT || NW <= 2 * NNS, "two lists per idle wave");
-    constexpr int nb = kRankSort<NT> ? 1 : bitonic_lds_stages(64 * NSW, 1);
+    constexpr int nb = bitonic_lds_stages(64 * NSW, 1);
     hyg_u128 n128 = hyg_u128_zero();
     hyg_u192 m192 = hyg_u192_zero();
     const int v = wave_id() - NSW;
