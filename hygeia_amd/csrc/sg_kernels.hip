@@ -903,12 +903,13 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       if (!PE) { SG_PH(17); }
       lds_barrier();
       if (!PE) { SG_PH(11); }
-      if (tid < K) {
-        const double m = mqv[tid];
-        double S = 0.0;
-#pragma unroll
-        for (int r = 0; r < K; ++r) {
-          const unsigned long long* el = Elimb + 3 * r;
+      if (wv == 0) {
+        // wave 0: lane r converts regime r's exact sum E_r once, lane q forms
+        // S_q = sum_r G[r][q] E_r with the E_r read across lanes (readlane, no
+        // LDS round trip per term), in r order as before (the same FMA chain)
+        double Er = 0.0;
+        if (lane < K) {
+          const unsigned long long* el = Elimb + 3 * lane;
           // E_r = l0 + l1 2^34 + l2 2^68 (each limb a sum of <= 256 values below 2^34)
           hyg_u128 e, x;
           e.lo = el[0]; e.hi = 0;
@@ -916,10 +917,20 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
           e = hyg_u128_add(e, x);
           x.lo = 0; x.hi = el[2] << 4;
           e = hyg_u128_add(e, x);
-          S = HYG_FMA(Gq[r * K + tid], hyg_u128_to_f64(e, 100), S);
+          Er = hyg_u128_to_f64(e, 100);
         }
-        lsev[tid] = (m > HYG_NINF) ? m + hyg_log(S) : HYG_NINF;  // log-normaliser of row q
-        lsev[K + tid] = (m > HYG_NINF) ? 1.0 / S : 0.0;
+        const int q = lane < K ? lane : 0;
+        double g[K];
+#pragma unroll
+        for (int r = 0; r < K; ++r) g[r] = Gq[r * K + q];
+        const double m = mqv[q];
+        double S = 0.0;
+#pragma unroll
+        for (int r = 0; r < K; ++r) S = HYG_FMA(g[r], d_of(rdlane64(u_of(Er), r)), S);
+        if (lane < K) {
+          lsev[lane] = (m > HYG_NINF) ? m + hyg_log(S) : HYG_NINF;  // log-normaliser of row q
+          lsev[K + lane] = (m > HYG_NINF) ? 1.0 / S : 0.0;
+        }
       }
       if (!PE) { SG_PH(18); }
       lds_barrier();

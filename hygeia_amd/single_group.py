@@ -29,7 +29,9 @@ libhygeia_amd.so; no CPU path). Reproduced quirks:
 
 Parity unpinned where R is the reference: R's RNG (arma::randn / the engine's
 streams) is not reproduced, and readr's number writer is replaced by Python's
-shortest round-trip text (the same values: `hygeia infer` reads theta exactly).
+shortest round-trip text (the same values), except in the theta file, written
+with 17 significant digits in exponent form so that `hygeia infer`'s pandas
+parser reads it within 3 ulp (write_vector).
 """
 from __future__ import annotations
 
@@ -239,9 +241,14 @@ def write_csv(path: str, header: Sequence[str], columns: Sequence[Sequence[str]]
         fh.write(text)
 
 
-def write_vector(path: str, name: str, values: Sequence[float]) -> None:
-    """write_to_csv_file(tibble(name = values)) (input_output_functions.R:4-7)."""
-    write_csv(path, [name], [[_shortest(v) for v in values]])
+def write_vector(path: str, name: str, values: Sequence[float], exp17: bool = False) -> None:
+    """write_to_csv_file(tibble(name = values)) (input_output_functions.R:4-7).
+    exp17: 17 significant digits in exponent form ('%.16e'), which pandas'
+    default parser -- `hygeia infer` reads the theta file with it, as
+    run_inference_two_groups.py:76-79 does -- reads within 3 ulp; the shortest
+    text of a small value ('0.00123...') has up to 21 mantissa characters, of
+    which it keeps 17 (errors of thousands of ulp, tests/test_single_group_cli.py)."""
+    write_csv(path, [name], [["%.16e" % v if exp17 else _shortest(v) for v in values]])
 
 
 def write_theta_trace(path: str, theta_rows: np.ndarray, n_sites: int, every: int) -> None:
@@ -373,7 +380,7 @@ def main(argv: Sequence[str]) -> int:
                   [[_shortest(v) for v in p_hat[:, c]] for c in range(K)])
         write_vector(f["omega_csv_file"], "omega", omega_hat)
         write_vector(f["kappa_csv_file"], "kappa", kappa)
-        write_vector(f["theta_file"], "data", last)
+        write_vector(f["theta_file"], "data", last, exp17=True)
     return 0
 
 

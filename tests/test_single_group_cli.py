@@ -120,3 +120,21 @@ def test_command_fails_loudly_without_a_gpu(tmp_path):
     assert e.value.code == _lib.HYG_EDEVICE
     assert (tmp_path / "out").is_dir()  # create_dirs_for_file ran first, as in the R script
     assert not (tmp_path / "out" / "regimes.csv.gz").exists()
+
+
+def test_theta_file_reads_back_through_pandas_within_3_ulp(tmp_path):
+    """The theta file is read by `hygeia infer` with pandas' default parser (as
+    run_inference_two_groups.py:76-79): its 17-digit exponent form comes back
+    within 3 ulp, where the shortest text of small values loses thousands."""
+    import pandas as pd
+
+    from hygeia_amd import cli
+
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.standard_normal(3000), rng.standard_normal(3000) * 1e-3])
+    sgc.write_vector(str(tmp_path / "theta_1.csv.gz"), "data", x, exp17=True)
+    y = cli.read_theta(str(tmp_path), "1")
+    assert np.all(np.abs(y - x) <= 3 * np.spacing(np.abs(x)))
+    sgc.write_vector(str(tmp_path / "theta_2.csv.gz"), "data", x)
+    z = pd.read_table(str(tmp_path / "theta_2.csv.gz"), sep=",")["data"].to_numpy()
+    assert np.max(np.abs(z - x) / np.spacing(np.abs(x))) > 100  # why the theta file is not written shortest

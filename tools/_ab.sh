@@ -1,4 +1,3 @@
-bash tools/gpu_run.sh r05c \
- "python bench.py --job c5 --steps 1 --warmup 1 --no-cpu-baseline" \
+bash tools/gpu_run.sh r05d \
  "HYG_LIB_PATH=hygeia_amd/lib/var_tuning/libhygeia_amd.so HYG_SG_PHASES=1 python tools/bench_sg.py --no-cpu-baseline --sites 4000000" \
  "python tools/bench_sg.py --no-cpu-baseline"
