@@ -609,13 +609,29 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       // ---- resampleCp (:406-450)
       if (N < Np + K) {
         bool keep_top = true;
+        // weights with a nonzero F = 100 image (order-free): each wave's count
+        // is published before the sort and read behind its cross-wave barriers
+        // (red's previous readers are behind the previous step's last barrier)
+        int* nzw = (int*)red + 2 * NW;
+        if (fin > M) {
+          const int wnz0 = __builtin_popcountll(wave_ballot(tid < Np && pw >= 0x1p-100));
+          if (lane == 0) nzw[wv] = wnz0;
+        }
         // order by log-weight (the keep-top fallback's order, Smc.h:432-441)
         uint64_t lkey = (tid < Np) ? sg_okey(plw) : 0;
         int lidx = tid;
         sg_bitonic<NB>(lkey, lidx, xk, xi);
         if (!PE) { SG_PH(12); }
         const double* wP = w_ + pb * NT;
+        int nz0 = 0;
         if (fin > M) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) nz0 += nzw[w];
+        }
+        // Fewer than M weights with a nonzero image: the K loop provably ends in
+        // the keep-top fallback (see below), so neither the order check nor the
+        // loop runs
+        if (fin > M && nz0 >= M) {
           // optimalFiniteState (resample.h:289-409) on the weights sorted
           // descending, ties by index. The log-weight order already is that
           // order when every adjacent pair along it has w decreasing, or w
@@ -835,6 +851,11 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         nst = sg_pack(sg_d(sa) + 1, r);
         nlw = lwres[tid] + (contP[a] + e);
       }
+      // the hazard parts of this thread's new particle (consumed next step):
+      // the L2 loads issued here, in flight through the weights' and the
+      // normalisation's barriers (fresh particle q = tid - M: state (1, q))
+      double nbase = HYG_NINF, ncont = HYG_NINF;
+      if (!PE && tid < N) sg_trans_parts(md, u, tid < M ? nst : sg_pack(1, tid - M), nbase, ncont);
       // backward kernels (:288-326), factorised over the regimes as in
       // oracle/sg_oracle.c: a_n = W_prev[n] + b_n (b_n + log P[r_n][q] = log
       // f((1,q) | n)), A_r = max of a_n over regime r, m_q = max_r (A_r + log
@@ -995,7 +1016,10 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         st_[cb * NT + tid] = my_st;
         lw_[cb * NT + tid] = my_lw;
         w_[cb * NT + tid] = my_w;
-        if (!PE) sg_trans_parts(md, u, my_st, my_base, my_cont);  // consumed next step
+        if (!PE) {  // (loaded with the weights)
+          my_base = nbase;
+          my_cont = ncont;
+        }
       }
       SG_PH(5);
       if constexpr (PE) {

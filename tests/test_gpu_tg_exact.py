@@ -194,3 +194,25 @@ def test_pipeline_k_backward_gpu_draws_follow_exact_smoother(oracle, K, T, dseed
         paths += [[(m[t, b], c[t, b, 0], c[t, b, 1], k[t, b, 0], k[t, b, 1]) for t in range(T)] for b in range(B)]
     n = draws_branch_counts(ex, paths)
     assert n[(2, True)] > 0 and n[(4, True)] > 0, dict(n)
+
+
+from test_tg_exact import PIPELINE_M50  # noqa: E402
+
+
+@pytest.mark.parametrize("K,T,M,dseed,u,S,cov", PIPELINE_M50)
+def test_pipeline_m50_resampling_gpu_unbiased_z(oracle, K, T, M, dseed, u, S, cov):
+    """The pipeline's M = 50 through the GPU's top-set resampling path (8 192
+    seeds in one launch): bit for bit the oracle (spot checks) and Z_hat / Z
+    unbiased against the exact enumeration."""
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2, u=u, S=S, cov=cov)
+    seeds = list(range(8192))
+    cid = 3
+    dc = _run_seeds(p, E, K, M, 2, seeds, cid)
+    for i in range(0, len(seeds), 511):
+        _check_chain_bits(oracle, p, E, dc, i, seeds[i], cid, T)
+    lz = dc.log_z.cpu().numpy()
+    zex = {r: ex.log_z(E_ex, r) for r in range(K)}
+    r = np.array([math.exp(lz[i] - zex[phantom_regime(oracle, s, cid, K)]) for i, s in enumerate(seeds)])
+    se = r.std() / math.sqrt(len(r))
+    assert abs(r.mean() - 1.0) < 4 * se + 1e-6, (r.mean(), se)
+    assert r.std() > 5e-4

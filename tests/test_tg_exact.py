@@ -362,3 +362,31 @@ def test_pipeline_k_resampling_keeps_z_unbiased(oracle, K, T, M, dseed, u, S):
     se = r.std() / math.sqrt(len(r))
     assert abs(r.mean() - 1.0) < 4 * se + 1e-3, (r.mean(), se, dict(modes))
     assert r.std() > 1e-3
+
+
+# The pipeline's M = 50 (run_inference_two_groups.py:37-39) with optimal
+# finite-state resampling active: K = 6, T = 8, weak data (coverage 3) so that
+# the resampling matters (Z_hat / Z spreads by ~1.5e-3). With M <= 64 the GPU
+# resamples these steps by its top-set path (A <= 256 of the N = 2 400
+# candidates, the cutoffs, the counting-sort fallback), so the GPU twin of this
+# test checks that path against the exact Z, not only against the oracle.
+# (K, T, M, data seed, u, samples per group, coverage)
+PIPELINE_M50 = [(6, 8, 50, 134, 3, 2, 3)]
+
+
+@pytest.mark.parametrize("K,T,M,dseed,u,S,cov", PIPELINE_M50)
+def test_pipeline_m50_resampling_keeps_z_unbiased(oracle, K, T, M, dseed, u, S, cov):
+    nseeds = 3000
+    p, ex, E, E_ex = _problem(oracle, K, T, dseed, M=M, B=2, u=u, S=S, cov=cov)
+    zex = {r: ex.log_z(E_ex, r) for r in range(K)}
+    ratios, modes = [], Counter()
+    for seed in range(nseeds):
+        out = oracle.chain(p, E, seed, 3, want_modes=True)
+        assert out["status"] == 0
+        modes.update((out["modes"][1:] // 65536).tolist())
+        ratios.append(math.exp(out["log_z"] - zex[phantom_regime(oracle, seed, 3, K)]))
+    assert modes[MODE_OPTIMAL] >= 3 * nseeds  # every chain resamples optimally on several steps
+    r = np.array(ratios)
+    se = r.std() / math.sqrt(len(r))
+    assert abs(r.mean() - 1.0) < 4 * se + 1e-6, (r.mean(), se, dict(modes))
+    assert r.std() > 5e-4  # the resampling adds variance: the test can see a bias
