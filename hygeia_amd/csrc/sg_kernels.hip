@@ -39,15 +39,26 @@ __device__ __forceinline__ int sg_r(uint32_t s) { return (int)(s >> 24); }
 // for d < u), and of the continuing particle (d + 1, r) it is cont =
 // log(1 - rho(d, r)). Both equal the oracle's sg_trans bit for bit (the
 // diagonal log P[r][r] = -inf covers q == r).
-__device__ __forceinline__ void sg_trans_parts(const SgModelDev& md, int u, uint32_t s, double& base,
-                                               double& cont) {
+// the hazard row and exit flag of state s (sg_trans_parts in two halves: the
+// loads, and the parts formed from them where they are used)
+__device__ __forceinline__ void sg_trans_load(const SgModelDev& md, uint32_t s, double2& h, uint8_t& ex) {
   const int d = sg_d(s), r = sg_r(s);
   int di = d - 1;
   if (di >= md.dcap) di = md.dcap - 1;
-  const double2 h = *(const double2*)(md.hz + ((size_t)r * md.dcap + di) * 2);
-  const uint8_t ex = md.ex[(size_t)r * md.dcap + di];
-  base = (d >= u) ? (ex ? 0.0 : h.x) : HYG_NINF;
+  h = *(const double2*)(md.hz + ((size_t)r * md.dcap + di) * 2);
+  ex = md.ex[(size_t)r * md.dcap + di];
+}
+__device__ __forceinline__ void sg_trans_form(int u, uint32_t s, const double2& h, uint8_t ex, double& base,
+                                              double& cont) {
+  base = (sg_d(s) >= u) ? (ex ? 0.0 : h.x) : HYG_NINF;
   cont = h.y;
+}
+__device__ __forceinline__ void sg_trans_parts(const SgModelDev& md, int u, uint32_t s, double& base,
+                                               double& cont) {
+  double2 h;
+  uint8_t ex;
+  sg_trans_load(md, s, h, ex);
+  sg_trans_form(u, s, h, ex, base, cont);
 }
 
 // ceil(T * R) for a double T in [0, 1] and R < 2^127 (oracle/sg_oracle.c:ceil_mul_f64)
@@ -854,8 +865,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       // the hazard parts of this thread's new particle (consumed next step):
       // the L2 loads issued here, in flight through the weights' and the
       // normalisation's barriers (fresh particle q = tid - M: state (1, q))
-      double nbase = HYG_NINF, ncont = HYG_NINF;
-      if (!PE && tid < N) sg_trans_parts(md, u, tid < M ? nst : sg_pack(1, tid - M), nbase, ncont);
+      double2 nh = make_double2(0.0, 0.0);
+      uint8_t nex = 0;
+      if (!PE && tid < N) sg_trans_load(md, tid < M ? nst : sg_pack(1, tid - M), nh, nex);
       // backward kernels (:288-326), factorised over the regimes as in
       // oracle/sg_oracle.c: a_n = W_prev[n] + b_n (b_n + log P[r_n][q] = log
       // f((1,q) | n)), A_r = max of a_n over regime r, m_q = max_r (A_r + log
@@ -1016,10 +1028,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         st_[cb * NT + tid] = my_st;
         lw_[cb * NT + tid] = my_lw;
         w_[cb * NT + tid] = my_w;
-        if (!PE) {  // (loaded with the weights)
-          my_base = nbase;
-          my_cont = ncont;
-        }
+        if (!PE) sg_trans_form(u, my_st, nh, nex, my_base, my_cont);  // (loaded with the weights)
       }
       SG_PH(5);
       if constexpr (PE) {
