@@ -62,6 +62,34 @@ __device__ __forceinline__ void sg_trans_parts(const SgModelDev& md, int u, uint
 }
 
 // ceil(T * R) for a double T in [0, 1] and R < 2^127 (oracle/sg_oracle.c:ceil_mul_f64)
+__device__ __forceinline__ hyg_u128 sg_ceil_mul_f64(double T, hyg_u128 R);
+// #{j in [0, L) : ceil(T_j R) <= v} for the systematic targets T_j = ((double)j
+// + uu) / (double)L (non-decreasing in j, as systematicBase forms them,
+// resample.h:85-117). The estimate jf = (v / R) L - uu lies within 2^-40 of the
+// crossing (the conversions and the division round at 2^-53, T_j at 2^-45 in
+// j units), so every j <= floor(jf) - 2 counts and no j >= floor(jf) + 2 does;
+// the three between are compared in f64 outside a 2^-40 relative guard band and
+// exactly (ceil(T_j R) <= v in integers) inside it.
+__device__ __forceinline__ int sg_sys_count(const hyg_u128& v, const hyg_u128& R, double invR, int L, double uu) {
+  const double y = hyg_u128_to_f64(v, 100) * invR;
+  double jf = y * (double)L - uu;
+  jf = jf < -2.0 ? -2.0 : (jf > (double)L + 2.0 ? (double)L + 2.0 : jf);
+  const int j0 = (int)floor(jf);
+  int c = j0 - 1;
+  c = c < 0 ? 0 : (c > L ? L : c);
+  const double ylo = y * (1.0 - 0x1p-40), yhi = y * (1.0 + 0x1p-40);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int j = j0 - 1 + k;
+    if (j >= 0 && j < L) {
+      const double T = ((double)j + uu) / (double)L;
+      bool le = T < ylo;
+      if (!le && !(T > yhi)) le = !hyg_u128_lt(v, sg_ceil_mul_f64(T, R));  // exact
+      c += le ? 1 : 0;
+    }
+  }
+  return c;
+}
 __device__ __forceinline__ hyg_u128 sg_ceil_mul_f64(double T, hyg_u128 R) {
   hyg_u128 z = hyg_u128_zero();
   if (!(T > 0.0)) return z;
@@ -102,6 +130,7 @@ struct SgShared {
   unsigned int lmask;  // free psi slots resident in LDS
   int pad1;
   double logC;
+  double uu;  // the step's systematic uniform, drawn ahead by an idle wave (512 threads)
   unsigned long long ph[kSgPh];  // phase timers (diagnostic runs only)
 };
 
@@ -627,6 +656,11 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         if (fin > M) {
           const int wnz0 = __builtin_popcountll(wave_ballot(tid < Np && pw >= 0x1p-100));
           if (lane == 0) nzw[wv] = wnz0;
+          // the systematic uniform of this step (systematicBase, resample.h:85-117), by
+          // the last wave, which holds no key (512 threads): off the residual's path
+          if (NB == 2 * NT && wv == NW - 1 && lane == 0)
+            sh.uu = (double)(hyg_rand64(ch.seed, ch.chain_id, kSgRngSystematic, (uint64_t)t, 0) >> 11) *
+                    1.1102230246251565404e-16;
         }
         // order by log-weight (the keep-top fallback's order, Smc.h:432-441)
         uint64_t lkey = (tid < Np) ? sg_okey(plw) : 0;
@@ -805,27 +839,33 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
                 // residual systematic draw (:372-377, systematicBase :85-117):
                 // T_j = (j + u) / L <= Q_i as exact C_i >= ceil(T_j R)
                 const bool inres = tid >= Kk && tid < Np;
-                const double rmax = block_max<NB>(inres ? lq : HYG_NINF, red);
+                // the residual's largest log q: with log q non-increasing along the
+                // sorted order (lqmono, checked for the K loop) it is position Kk's
+                const double rmax = lqmono ? logq[Kk] : block_max<NB>(inres ? lq : HYG_NINF, red);
                 const hyg_u128 m2 = inres ? hyg_exp_fix100(lq - rmax) : hyg_u128_zero();
                 block_scan128<NB>(m2, cum, red);
-                const hyg_u128 incl = hyg_u128_add(cum[tid], m2);
+                const hyg_u128 exv = cum[tid];  // C(p - 1) at sorted position p = tid
+                const hyg_u128 incl = hyg_u128_add(exv, m2);
                 lds_barrier();
                 cum[tid] = incl;
                 lds_barrier();
                 const hyg_u128 R = cum[Np - 1];
-                if (tid < L) {
+                if (inres) {
+                  // target j lands on the first position p >= Kk with C(p) >= ceil(T_j R):
+                  // position p takes the targets j in [count(C(p - 1)), count(C(p)))
+                  // (position Kk from j = 0), counted per position instead of
+                  // searched per target
                   const double uu =
-                      (double)(hyg_rand64(ch.seed, ch.chain_id, kSgRngSystematic, (uint64_t)t, 0) >> 11) *
-                      1.1102230246251565404e-16;
-                  const double Tj = ((double)tid + uu) / (double)L;
-                  const hyg_u128 thr = sg_ceil_mul_f64(Tj, R);
-                  int lo = Kk, hi = Np - 1;
-                  while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (hyg_u128_lt(cum[mid], thr)) lo = mid + 1; else hi = mid;
+                      (NB == 2 * NT) ? sh.uu
+                                     : (double)(hyg_rand64(ch.seed, ch.chain_id, kSgRngSystematic, (uint64_t)t, 0) >> 11) *
+                                           1.1102230246251565404e-16;
+                  const double invR = 1.0 / hyg_u128_to_f64(R, 100);
+                  const int cHi = sg_sys_count(incl, R, invR, L, uu);
+                  const int cLo = (tid == Kk) ? 0 : sg_sys_count(exv, R, invR, L, uu);
+                  for (int j = cLo; j < cHi; ++j) {
+                    anc[Kk + j] = idx;
+                    lwres[Kk + j] = logZp - logC;
                   }
-                  anc[Kk + tid] = sidx[lo];
-                  lwres[Kk + tid] = logZp - logC;
                 }
               }
             }
