@@ -6,7 +6,7 @@
 #   rocprofv3 profile set of the default workload (tools/gpu_profile.sh).
 # Outputs: gpurun_out/<tag>/* (only gpurun_out/ comes back from the box; copy
 # gpurun_out/<tag>/out/* and gpurun_out/prof_<tag>/* into profiles/ afterwards).
-# usage: bash tools/gpu_final.sh <tag>
+# usage: bash tools/gpu_final.sh <tag> [no-profile]
 set -u
 export TMPDIR=/tmp
 tag=$1
@@ -39,10 +39,14 @@ fi
 step bench_c2 600 python tools/bench_sg.py
 step bench_c1 600 python tools/bench_sg.py --config c1
 step bench_pipe 600 python tools/bench_pipeline.py
-bash tools/gpu_profile.sh $tag > $O/profile.log 2>&1; rc=$?
-tail -5 $O/profile.log
+step bench_pipe_concurrent 600 python tools/bench_pipeline.py --concurrent 8,16
+rc=0
+if [ "${2:-}" != "no-profile" ]; then  # (the profile set can run as its own call: bash tools/gpu_profile.sh <tag>)
+  bash tools/gpu_profile.sh $tag > $O/profile.log 2>&1; rc=$?
+  tail -5 $O/profile.log
+fi
 mkdir -p $O/out
-for n in bench_c3 bench_c4 bench_c5 bench_c3_shard0of8 bench_c4_shard0of8 bench_c2 bench_c1 bench_pipe; do
+for n in bench_c3 bench_c4 bench_c5 bench_c3_shard0of8 bench_c4_shard0of8 bench_c2 bench_c1 bench_pipe bench_pipe_concurrent; do
   grep '^{' $O/$n.log | tail -1 > $O/out/${tag}_$n.json
 done
 grep -h "phases" $O/phases_c3_shard0of8.log > $O/out/${tag}_phases_c3_shard0of8.log 2>/dev/null
