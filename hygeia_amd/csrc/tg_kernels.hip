@@ -550,43 +550,20 @@ __device__ __forceinline__ void gen_weights(const ConstLds& cl, int K, int I, in
         }
       }
       // two change points (i, j): x = (i == j, 1, i, 1, j), from the wave's
-      // first slot >= 2K. In batches of kTG slots, every LDS read of a batch
-      // (the emission rows of i and j, row r_c of log P_ctrl at i) issued
-      // before its first weight store, and the batch branch-free: a store (or
-      // a slot bound check) between two slots' reads made each slot wait out its
-      // own LDS round trip (the reads may alias W). A wave with one slot fewer
-      // (NW does not divide K^2) repeats its first slot in the last position:
-      // the same value stored again to the same place, not counted.
-      constexpr int kTG = NT >= 512 ? 6 : 3;
+      // first slot >= 2K
       const int s0 = wv + NW * ((K2 - wv + NW - 1) / NW);
-      const int nts = (I - K2 + NW - 1) / NW;  // two-change slots of a wave (some waves one fewer)
-      if (s0 < I) {  // (uniform: every wave but those of K = 2 past the last slot)
 #pragma unroll
-        for (int k0 = 0; k0 < nts; k0 += kTG) {
-          double eb[kTG], lcb[kTG];
-          int sb[kTG];
-          bool vb[kTG];
-#pragma unroll
-          for (int g = 0; g < kTG; ++g) {
-            const int sg = s0 + (k0 + g) * NW;
-            vb[g] = k0 + g < nts && sg < I;
-            sb[g] = vb[g] ? sg : s0;
-            const int ii = (sb[g] - K2) / K, jj = (sb[g] - K2) - ii * K;
-            eb[g] = Et[ii] + Et[K + jj];
-            lcb[g] = h.lrc + lPcr[ii];
-          }
-#pragma unroll
-          for (int g = 0; g < kTG; ++g) {
-            const int ii = (sb[g] - K2) / K, jj = (sb[g] - K2) - ii * K;
-            const double lkch = (jj != ark) ? (h.lrk + ((ii == ark) ? q.lU1 : q.lU2)) : NINF;
-            const double lk = (ii == jj) ? 0.0 : ((ii == ark && am == 0) ? q.lU1 : lkch);
-            const double tr = (((ii == jj) ? lm1 : lm0) + lcb[g]) + lk;
-            const double w = hyg_isfinite(tr) ? (base + (tr + eb[g])) - sub : NINF;
-            W[sb[g] * np + lane] = w;
-            m = dmax(m, w);
-            cnt += (vb[g] && w > NINF) ? 1 : 0;
-          }
-        }
+      for (int k = 0; k < (I - K2 + NW - 1) / NW; ++k) {
+        const int s = s0 + k * NW;
+        if (s >= I) break;
+        const int ii = (s - K2) / K, jj = (s - K2) - ii * K;
+        const double e = Et[ii] + Et[K + jj];
+        const double lc = h.lrc + lPcr[ii];
+        double lk;
+        if (ii == jj) lk = 0.0;
+        else if (ii == ark && am == 0) lk = q.lU1;
+        else lk = (jj != ark) ? (h.lrk + ((ii == ark) ? q.lU1 : q.lU2)) : NINF;
+        put(s, (((ii == jj) ? lm1 : lm0) + lc) + lk, e);
       }
     }
     *m_out = m;
