@@ -380,6 +380,11 @@ int hyg_tg_force_threads(int32_t forward, int32_t backward) {
   return rc == HYG_OK ? rc : fail(rc, "unsupported workgroup size");
 }
 
+int hyg_sg_force_key_drop(int32_t bits) {
+  const int rc = hyg::sg_force_key_drop(bits);
+  return rc == HYG_OK ? rc : fail(rc, "key bits out of range [8, 60]");
+}
+
 int hyg_tg_emission(const hyg_tg_model* m, const uint16_t* meth_c, const uint16_t* tot_c, int32_t s_c,
                     const uint16_t* meth_k, const uint16_t* tot_k, int32_t s_k, int64_t n_sites, double* E,
                     void* stream) {

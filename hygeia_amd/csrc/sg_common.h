@@ -25,6 +25,7 @@ struct SgModelDev {
   const double* lf;             // BB tables as hyg_sg_bb_tables
   const double* lg;
   const double* cst;
+  uint64_t key_keep;            // the packed log-weight sort's key bits (~0xff; hyg_sg_force_key_drop)
 };
 
 struct SgChainDev {
@@ -90,6 +91,7 @@ __host__ __device__ inline size_t sg_chain_ws_bytes(int K, int cap) {
 int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint16_t* meth, const uint16_t* tot,
                        int S, int64_t n_sites, double* E, void* stream);
 // ctl: the chains' ring control words (kSgCtlBytes each, contiguous), zeroed here before the launches
+int sg_force_key_drop(int bits);  // test override of the packed sort's dropped key bits (0 = 8)
 int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
                      const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* ctl,
                      void* stream, const SgPeDev* pe = nullptr);

@@ -130,7 +130,13 @@ struct SgShared {
   unsigned int lmask;  // free psi slots resident in LDS
   int pad1;
   double logC;
-  double uu;  // the step's systematic uniform, drawn ahead by an idle wave (512 threads)
+  // the systematic uniforms of steps 64 j .. 64 j + 63, drawn one block ahead
+  // by an idle wave, one step per lane (512 threads)
+  double uring[64];
+  // keep-top steps: each key wave's first and last full log-weight key and index
+  // after the packed sort, and whether an in-wave pair is out of order
+  unsigned long long kfirst[4], klast[4];
+  int ifirst[4], ilast[4], kbad[4];
   unsigned long long ph[kSgPh];  // phase timers (diagnostic runs only)
 };
 
@@ -469,6 +475,62 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
   }
 }
 
+// The same network on one 64-bit word per thread: the log-weight key's top 56
+// bits with 255 - idx in the low byte, so ties of the word order by ascending
+// idx and a compare-exchange is one 64-bit compare and two selects (the pair
+// sort above: three compares, their merge and three selects). Descending words
+// are the pair order except inside a run of keys that agree on the top 56 bits
+// and differ below them; the caller checks the order it uses (sg_chain_kernel).
+template <int NB>
+__device__ __forceinline__ void sg_bitonic_packed(uint64_t& key, uint64_t* xk) {
+  constexpr int NT = kSgThreads;
+  const int tid = threadIdx.x;
+  const bool real = (NB == NT) || tid < NT;
+  int buf = 0;
+#pragma unroll
+  for (int k = 2; k <= NT; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint64_t pk = key;
+      if (j >= 64) {
+        if (real) xk[buf * NB + tid] = key;
+        lds_barrier();
+        if (real) pk = xk[buf * NB + (tid ^ j)];
+        buf ^= 1;
+      } else if (real) {
+        switch (j) {
+          case 1: pk = xshfl64<1>(key); break;
+          case 2: pk = xshfl64<2>(key); break;
+          case 4: pk = xshfl64<4>(key); break;
+          case 8: pk = xshfl64<8>(key); break;
+          case 16: pk = xshfl64<16>(key); break;
+          default: pk = xshfl64<32>(key); break;
+        }
+      }
+      if (j < 64) {
+        if (real) {
+          const uint64_t lower = lanes_bit_clear(j);
+          const uint64_t same = (k < 64) ? ~(lower ^ lanes_bit_clear(k < 64 ? k : 1))
+                                         : (((wave_id() * 64) & k) == 0 ? lower : ~lower);
+          const uint64_t take = ~(same ^ wave_ballot(pk > key));
+          key = lane_select64(take, key, pk);
+        }
+      } else if (real) {
+        const bool up = (tid & k) == 0, lower = (tid & j) == 0;
+        if ((lower == up) ? (pk > key) : !(pk > key)) key = pk;
+      }
+    }
+  }
+}
+__device__ __forceinline__ uint64_t sg_pack_key(uint64_t okey, int idx, uint64_t keep) {
+  return (okey & keep) | (uint64_t)(255 - idx);
+}
+__device__ __forceinline__ int sg_packed_idx(uint64_t key) { return 255 - (int)(key & 0xffull); }
+// the value of the lane above (DPP wave_shl:1; lane 63 gets 0)
+__device__ __forceinline__ uint32_t sg_lane_next(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+
 // One workgroup per chain, thread n = particle n (N_max <= 256). Per step the
 // critical path is a few dozen barriers: sorts in registers, the K / log c
 // fixed point in one wave, batched reductions for the K fresh-particle rows
@@ -631,6 +693,14 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
   for (int t = 0; t < T; ++t) {
     const int cb = t & 1, pb = cb ^ 1;  // LDS buffers of the current / previous particle sets
     int M = 0, Np = N;
+    bool check_top = false;  // a keep-top step: its order is confirmed behind the barrier
+    // this thread's ancestor and resampled log-weight (tid < M) when the thread
+    // chose them itself (keep-top, no resampling): read from registers, not
+    // back from LDS behind the barrier; the optimal branch spreads them over
+    // the threads (anc_lds)
+    int my_anc = tid;
+    double my_lwr = HYG_NINF;
+    bool anc_lds = false;
     if (t > 0) {
       // ---- Smc::iterate (:190-286): the current set becomes the previous one
       const uint32_t* stP = st_ + pb * NT;
@@ -645,6 +715,15 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       const uint32_t pst = my_st;
       N = (Np + K > Nmax) ? Nmax : Np + K;
       M = N - K;
+      // the systematic uniforms (systematicBase, resample.h:85-117) of steps
+      // 64 j .. 64 j + 63, at the block's first step, by the last wave, which
+      // holds no particle (512 threads): lane l draws step 64 j + l while the
+      // key waves sort (read behind the sort's barriers; the previous block's
+      // last reader is behind the previous step's barriers)
+      if (NB == 2 * NT && wv == NW - 1 && (t == 1 || (t & 63) == 0))
+        sh.uring[lane] =
+            (double)(hyg_rand64(ch.seed, ch.chain_id, kSgRngSystematic, (uint64_t)((t & ~63) + lane), 0) >> 11) *
+            1.1102230246251565404e-16;
       SG_PH(0);
       // ---- resampleCp (:406-450)
       if (N < Np + K) {
@@ -656,16 +735,13 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         if (fin > M) {
           const int wnz0 = __builtin_popcountll(wave_ballot(tid < Np && pw >= 0x1p-100));
           if (lane == 0) nzw[wv] = wnz0;
-          // the systematic uniform of this step (systematicBase, resample.h:85-117), by
-          // the last wave, which holds no key (512 threads): off the residual's path
-          if (NB == 2 * NT && wv == NW - 1 && lane == 0)
-            sh.uu = (double)(hyg_rand64(ch.seed, ch.chain_id, kSgRngSystematic, (uint64_t)t, 0) >> 11) *
-                    1.1102230246251565404e-16;
         }
-        // order by log-weight (the keep-top fallback's order, Smc.h:432-441)
-        uint64_t lkey = (tid < Np) ? sg_okey(plw) : 0;
-        int lidx = tid;
-        sg_bitonic<NB>(lkey, lidx, xk, xi);
+        // order by log-weight (the keep-top fallback's order, Smc.h:432-441), on
+        // packed words: exact wherever the order is used (the optimal branch
+        // re-checks it against w below, the keep-top path with the full keys)
+        uint64_t lkey = sg_pack_key((tid < Np) ? sg_okey(plw) : 0, tid & (NT - 1), md.key_keep);
+        sg_bitonic_packed<NB>(lkey, xk);
+        const int lidx = sg_packed_idx(lkey);
         if (!PE) { SG_PH(12); }
         const double* wP = w_ + pb * NT;
         int nz0 = 0;
@@ -830,6 +906,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
             const double logC = sh.logC;
             if (hyg_isfinite(logC)) {
               keep_top = false;
+              anc_lds = true;
               const int Kk = sh.Kk, L = M - Kk;
               if (tid < Kk) {
                 anc[tid] = idx;
@@ -856,7 +933,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
                   // (position Kk from j = 0), counted per position instead of
                   // searched per target
                   const double uu =
-                      (NB == 2 * NT) ? sh.uu
+                      (NB == 2 * NT) ? sh.uring[t & 63]
                                      : (double)(hyg_rand64(ch.seed, ch.chain_id, kSgRngSystematic, (uint64_t)t, 0) >> 11) *
                                            1.1102230246251565404e-16;
                   const double invR = 1.0 / hyg_u128_to_f64(R, 100);
@@ -871,16 +948,47 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
             }
           }
         }
-        if (keep_top && tid < M) {
-          // keep the M largest log-weights (Smc.h:432-441, resample.h:379-384)
-          anc[tid] = lidx;
-          lwres[tid] = lwP[lidx];
+        if (keep_top) {
+          // keep the M largest log-weights (Smc.h:432-441, resample.h:379-384).
+          // The packed words order keys that agree on their top 56 bits by
+          // index: every adjacent pair of real positions is checked with the
+          // full keys, the pairs inside a wave here, the three across waves
+          // behind the barrier below (then the exact pair sort redoes it).
+          uint64_t fk = 0;
+          double flw = HYG_NINF;
+          if (tid < Np) {
+            flw = lwP[lidx];
+            fk = sg_okey(flw);
+          }
+          if (tid < M) {
+            anc[tid] = lidx;
+            lwres[tid] = flw;
+          }
+          if (tid < NT) {
+            const uint64_t nk = ((uint64_t)sg_lane_next((uint32_t)(fk >> 32)) << 32) | sg_lane_next((uint32_t)fk);
+            const int ni = (int)sg_lane_next((uint32_t)lidx);
+            const bool bad = lane < 63 && tid + 1 < Np && !(fk > nk || (fk == nk && lidx < ni));
+            const int wbad = wave_ballot(bad) != 0 ? 1 : 0;
+            if (lane == 0) {
+              sh.kfirst[wv] = fk;
+              sh.ifirst[wv] = lidx;
+              sh.kbad[wv] = wbad;
+            }
+            if (lane == 63) {
+              sh.klast[wv] = fk;
+              sh.ilast[wv] = lidx;
+            }
+          }
+          check_top = true;
+          my_anc = lidx;
+          my_lwr = flw;
         }
         SG_CNT(8, keep_top ? 0 : 1);
         SG_CNT(9, keep_top ? 1 : 0);
       } else if (tid < M) {
         anc[tid] = tid;
         lwres[tid] = plw;
+        my_lwr = plw;
       }
       // the weights' LDS accumulators, behind this barrier (their last readers
       // were behind the previous step's last barrier; block reductions do not
@@ -888,19 +996,56 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       if (tid < K) Amax[tid] = HYG_NINF;
       if (tid < 3 * K) Elimb[tid] = 0ull;
       lds_barrier();
+      if (check_top) {
+        // every value loaded first (one LDS round trip), then a branch-free test
+        constexpr int KW = NT / 64;
+        uint64_t kf[KW], kl[KW];
+        int jf[KW], jl[KW], kb[KW];
+#pragma unroll
+        for (int w = 0; w < KW; ++w) {
+          kf[w] = sh.kfirst[w];
+          kl[w] = sh.klast[w];
+          jf[w] = sh.ifirst[w];
+          jl[w] = sh.ilast[w];
+          kb[w] = sh.kbad[w];
+        }
+        int redo = 0;
+#pragma unroll
+        for (int w = 0; w < KW; ++w) {
+          redo |= kb[w];
+          if (w + 1 < KW) {
+            const uint64_t a = kl[w], b = kf[w + 1];
+            const bool ok = (a > b) | ((a == b) & (jl[w] < jf[w + 1]));
+            redo |= (64 * (w + 1) < Np && !ok) ? 1 : 0;
+          }
+        }
+        if (redo != 0) {  // uniform: the exact pair sort
+          uint64_t key = (tid < Np) ? sg_okey(plw) : 0;
+          int idx = tid;
+          sg_bitonic<NB>(key, idx, xk, xi);
+          my_anc = idx;
+          my_lwr = (tid < Np) ? lwP[idx] : HYG_NINF;
+          if (tid < M) {
+            anc[tid] = my_anc;
+            lwres[tid] = my_lwr;
+          }
+          lds_barrier();
+          SG_CNT(22, 1);
+        }
+      }
       SG_PH(3);
       // ---- sampleParticlesCp (:504-522) + computeWeightsCp (:536-574)
       double nlw = HYG_NINF;
       uint32_t nst = 0;
       if (tid < M) {
-        const int a = anc[tid];
+        const int a = anc_lds ? anc[tid] : my_anc;
         const uint32_t sa = stP[a];
         const int r = sg_r(sa);
         double e = et[0];
 #pragma unroll
         for (int q = 1; q < K; ++q) e = (r == q) ? et[q] : e;
         nst = sg_pack(sg_d(sa) + 1, r);
-        nlw = lwres[tid] + (contP[a] + e);
+        nlw = (anc_lds ? lwres[tid] : my_lwr) + (contP[a] + e);
       }
       // the hazard parts of this thread's new particle (consumed next step):
       // the L2 loads issued here, in flight through the weights' and the
@@ -1599,10 +1744,21 @@ int sg_launch_emission(const SgModelDev& md, const hyg_sg_consts& c, const uint1
 }
 
 
-int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
+// The packed sort keeps the top 64 - g_key_drop bits of a key (8 in production;
+// tests drop more, so that keys collide and the exact re-sort runs often)
+static int g_key_drop = 8;
+int sg_force_key_drop(int bits) {
+  if (bits != 0 && (bits < 8 || bits > 60)) return HYG_EINVAL;
+  g_key_drop = bits ? bits : 8;
+  return HYG_OK;
+}
+
+int sg_launch_chains(const SgModelDev& md_in, const hyg_sg_consts& c, const SgChainDev* chains_dev, int n_chains,
                      const double* E, uint8_t* ws, int psi_cap, double* probs, int32_t* status, void* ctl,
                      void* stream, const SgPeDev* pe) {
   if (n_chains <= 0) return HYG_OK;
+  SgModelDev md = md_in;
+  md.key_keep = ~((1ull << g_key_drop) - 1ull);
   if (c.Nmax > kSgThreads || c.K < 2 || c.K > HYG_KMAX) return HYG_EUNSUPPORTED;
   const SgLay lay = sg_layout(c.K, psi_cap, pe != nullptr);
   const SgCLay clay = sg_clayout(c.K, psi_cap);
@@ -1680,8 +1836,8 @@ int sg_launch_chains(const SgModelDev& md, const hyg_sg_consts& c, const SgChain
               (double)hl[14] / std::max(1.0, steps / (double)pe->c.every));
       sum += v(12) + v(13);
     }
-    fprintf(stderr, " total=%.0f | optimal=%.0f keep_top=%.0f kloop_iters/capped=%.2f\n", sum, (double)hl[8],
-            (double)hl[9], (double)hl[10] / std::max(1.0, (double)(hl[8] + hl[9])));
+    fprintf(stderr, " total=%.0f | optimal=%.0f keep_top=%.0f kloop_iters/capped=%.2f keep_top_resorts=%.0f\n", sum,
+            (double)hl[8], (double)hl[9], (double)hl[10] / std::max(1.0, (double)(hl[8] + hl[9])), (double)hl[22]);
   }
   return HYG_OK;
 }

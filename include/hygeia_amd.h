@@ -135,6 +135,14 @@ size_t hyg_tg_lds_bytes(const hyg_tg_model* model, int32_t threads, int32_t back
  * on it: every width computes the same bits. */
 int hyg_tg_force_threads(int32_t forward, int32_t backward);
 
+/* Test override of the single-group chain's log-weight sort for every later
+ * launch in the process. The sort orders one 64-bit word per particle: the
+ * order key's top 64 - bits bits and the particle index (bits = 8, or 0 for
+ * the default). Wherever keys that agree on those bits disagree below them,
+ * the kernel detects it and re-sorts exactly, so the results do not depend on
+ * it; larger values (up to 60) make that path run often. Not thread-safe. */
+int hyg_sg_force_key_drop(int32_t bits);
+
 /* Per-site emission table E[t][g*K + r] = log g_t for group g (0 control,
  * 1 case) and regime r: sum over samples of BetaBinomial(meth | total,
  * alpha_r, beta_r) (case_control_regime_model.py:197-231). Counts are

@@ -108,6 +108,34 @@ def test_chain_bit_exact(lib, sg, K, T, S, cov, dseed, Nmax, eps, u, seed):
     assert bad.size == 0, (bad[:5], out[tuple(bad[0])], ref["regime_probs"][tuple(bad[0])])
 
 
+@pytest.mark.parametrize("drop", [40, 52])
+def test_packed_sort_collisions_resort_exactly(lib, sg, drop):
+    """The chain's log-weight sort orders one word per particle: the order key's
+    top bits and the index. Keys that agree on those bits but not below them
+    are caught (the keep-top path checks every adjacent pair with the full keys
+    and re-sorts exactly; the optimal branch re-checks the order against w).
+    With `drop` low bits dropped instead of 8 (hyg_sg_force_key_drop; 52 keeps
+    only the sign and exponent) keys collide on most steps, so both checks
+    carry the order, and every chain stays bit-exact."""
+    for K, T, S, cov, dseed, Nmax, eps, u, seed in (CASES[0], CASES[1], CASES[2], CASES[9]):
+        meth, tot, mu, sgm = _data(K, T, S, cov, dseed, u=u)
+        omega = sg.DEFAULT_OMEGA if K == 6 else [0.93] * K
+        p = sg.make_params(K=K, mu=mu, sigma=sgm, P=_uniform_P(K), omega=omega, u=u, Nmax=Nmax, epsilon=eps)
+        ref = sg.chain(p, sg.emission(p, meth, tot), seed=seed, chain_id=(3 << 32) | seed)
+        assert ref["status"] == 0
+        m = Model(lib, p, max(int(tot.max()), 1), T + 10)
+        assert lib.hyg_sg_force_key_drop(drop) == 0
+        try:
+            rc, out = m.chain_host(meth, tot, seed, (3 << 32) | seed)
+            assert rc == 0, lib.hyg_last_error()
+        finally:
+            lib.hyg_sg_force_key_drop(0)
+            m.close()
+        bad = np.argwhere(out != ref["regime_probs"])
+        assert bad.size == 0, (K, T, bad[:5])
+    assert lib.hyg_sg_force_key_drop(7) != 0 and lib.hyg_sg_force_key_drop(61) != 0
+
+
 def test_golden_fixtures(lib, sg):
     for name in ("sg_chain_k6", "sg_chain_k3"):
         g = np.load(os.path.join(GOLDEN, name + ".npz"))

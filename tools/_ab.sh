@@ -1,10 +1,9 @@
 P=hygeia_amd/lib/var_prev/libhygeia_amd.so
 T=hygeia_amd/lib/var_tuning/libhygeia_amd.so
-bash tools/gpu_run.sh r05i \
- "python bench.py --shard 0/8 --no-cpu-baseline --steps 2" \
- "HYG_LIB_PATH=$P python bench.py --shard 0/8 --no-cpu-baseline --steps 2" \
- "python bench.py --job c5 --steps 1 --warmup 1 --no-cpu-baseline" \
- "HYG_LIB_PATH=$P python bench.py --job c5 --steps 1 --warmup 1 --no-cpu-baseline" \
- "python bench.py --no-cpu-baseline" \
- "HYG_LIB_PATH=$P python bench.py --no-cpu-baseline" \
- "HYG_LIB_PATH=$T HYG_DEBUG_PHASES=1 python bench.py --job c5 --steps 1 --warmup 0 --no-cpu-baseline"
+bash tools/gpu_run.sh r05n \
+ "python tools/bench_sg.py" \
+ "HYG_LIB_PATH=$P python tools/bench_sg.py" \
+ "python tools/bench_sg.py --config c1" \
+ "HYG_LIB_PATH=$P python tools/bench_sg.py --config c1" \
+ "HYG_LIB_PATH=$T HYG_SG_PHASES=1 python tools/bench_sg.py" \
+ "HYG_LIB_PATH=hygeia_amd/lib/var_prevtune/libhygeia_amd.so HYG_SG_PHASES=1 python tools/bench_sg.py"
