@@ -404,11 +404,11 @@ __host__ __device__ inline Lay make_layout(int K, int M, int B, int Nmax, int NT
   }
   l.red = o; o = align_up(o + 2 * 32 * (NT / 64), 16);  // two slots: the step's log-sum-exp has its own
   l.sh = o; o = align_up(o + sizeof(Shared), 16);
-  // the forward at one chain per CU (NT >= 512): the systematic uniforms of the
-  // next 64 steps, drawn 64 at a time (not at 256 threads: three chains per CU
-  // leave its layout ~240 B of LDS)
+  // the forward's systematic uniforms of the next 64 steps, drawn 64 at a time
+  // (NT >= 512: one chain per CU); 32 at 256 threads, whose three chains per CU
+  // leave the layout ~240 B of LDS
   l.uring = o;
-  if (!backward && NT >= 512) o = align_up(o + sizeof(float) * 64, 16);
+  if (!backward && NT >= 256) o = align_up(o + sizeof(float) * (NT >= 512 ? 64 : 32), 16);
   l.total = o;
   return l;
 }
@@ -1648,8 +1648,9 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
   int* parents = (int*)(smem + lay.parents);
   unsigned char* red = smem + lay.red;
   Shared& sh = *(Shared*)(smem + lay.sh);
-  float* uring = (float*)(smem + lay.uring);  // NT >= 512 only (kURing)
-  constexpr bool kURing = NT >= 512;
+  float* uring = (float*)(smem + lay.uring);  // NT >= 256 only (kURing)
+  constexpr bool kURing = NT >= 256;
+  constexpr int kUR = NT >= 512 ? 64 : 32;  // ring entries
   int* part_cnt = (int*)(smem + lay.part);
   hyg_u192* part_tot = (hyg_u192*)(smem + lay.part + sizeof(int) * kNCut * (NT / 64));
 
@@ -1678,8 +1679,8 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
     StepScalars* s0 = (StepScalars*)rec0;
     s0->mode = MODE_INIT; s0->n_par = 0; s0->log_c = 0.0f; s0->r_ph = sh.r_ph; s0->lse = 0.0; s0->pad = 0.0;
   }
-  if (kURing && wave_id() == NT / 64 - 1)  // steps 1 .. 64
-    uring[(1 + lane_id()) & 63] =
+  if (kURing && wave_id() == NT / 64 - 1 && lane_id() < kUR)  // steps 1 .. kUR
+    uring[(1 + lane_id()) & (kUR - 1)] =
         hyg_u01f(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)(1 + lane_id()), 0));
   lds_barrier();
   double mloc;
@@ -1705,8 +1706,8 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       if (tid == 0) sh.status = HYG_ENUMERIC;
       break;  // uniform
     }
-    // written during step t-1's gather (or, kURing, a multiple of 64 steps ago), before two barriers
-    const float Ucur = kURing ? uring[t & 63] : sh.Unext;
+    // written during step t-1's gather (or, kURing, a multiple of kUR steps ago), before two barriers
+    const float Ucur = kURing ? uring[t & (kUR - 1)] : sh.Unext;
     // ---- log_softmax / reduce_logsumexp of the weights of step t-1
     // ---- per wave, the list of candidates with W - mx >= sig_thresh (keys
     //      area): every nonzero F=100 mass (x >= -70) and every significant
@@ -1943,9 +1944,9 @@ tg_forward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const double
       rs->mode = mode; rs->n_par = np; rs->log_c = log_c; rs->r_ph = 0; rs->lse = lse; rs->pad = 0.0;
     }
     if (wave_id() == 0) serial_end();
-    if (kURing) {  // steps t+1 .. t+64, one per lane, every 64 steps (step t's entry was read above)
-      if (wave_id() == NT / 64 - 1 && (t & 63) == 0)
-        uring[(t + 1 + lane_id()) & 63] =
+    if (kURing) {  // steps t+1 .. t+kUR, one per lane, every kUR steps (step t's entry was read above)
+      if (wave_id() == NT / 64 - 1 && (t & (kUR - 1)) == 0 && lane_id() < kUR)
+        uring[(t + 1 + lane_id()) & (kUR - 1)] =
             hyg_u01f(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)(t + 1 + lane_id()), 0));
     } else if (wave_id() == NT / 64 - 1) {  // a wave with no ancestor (when NT > M): next step's uniform
       const float un = hyg_u01f(hyg_rand64(ch.seed, ch.chain_id, HYG_RNG_SYSTEMATIC, (uint64_t)(t + 1), 0));

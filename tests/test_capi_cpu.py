@@ -116,15 +116,17 @@ def test_compute_refuses_without_device(lib):
 
 def test_pipeline_shape_lds_stays_under_the_three_per_cu_boundary(lib):
     """C3 on one GPU holds three 256-thread forward chains per CU. The forward's
-    LDS at the pipeline shape (K = 6, M = 50, B = 25) is 53 520 B, which fits three
-    times; 256 B more (53 776 B) measured two per CU on the MI355X while the HIP
-    occupancy query still said three (C3 forward 1957 -> 2887 ms, profiles/r04s).
-    Growing the 256-thread layout needs a GPU check of C3 first."""
+    LDS at the pipeline shape (K = 6, M = 50, B = 25) is 53 648 B (53 520 B and a
+    32-entry uniform ring, round 5), which fits three times (C3 forward 1973 ->
+    1907 ms, profiles/r05p_uring256_ab.txt); 53 776 B measured two per CU on the
+    MI355X while the HIP occupancy query still said three (C3 forward 1957 ->
+    2887 ms, profiles/r04s). Growing the 256-thread layout needs a GPU check of C3
+    first."""
     m = C.c_void_p()
     assert lib.hyg_tg_model_create(C.byref(_params()), 200, 1000, C.byref(m)) == _lib.HYG_OK
     try:
         fwd256 = lib.hyg_tg_lds_bytes(m, 256, 0)
-        assert 0 < fwd256 <= 53520
+        assert 0 < fwd256 <= 53648
         assert 3 * lib.hyg_tg_lds_bytes(m, 256, 1) <= 160 * 1024  # the backward at three per CU
         for nt in (512, 768):  # one chain per CU
             assert 0 < lib.hyg_tg_lds_bytes(m, nt, 0) <= 160 * 1024
