@@ -6,7 +6,9 @@
 #   rocprofv3 profile set of the default workload (tools/gpu_profile.sh).
 # Outputs: gpurun_out/<tag>/* (only gpurun_out/ comes back from the box; copy
 # gpurun_out/<tag>/out/* and gpurun_out/prof_<tag>/* into profiles/ afterwards).
-# usage: bash tools/gpu_final.sh <tag> [no-profile]
+# usage: bash tools/gpu_final.sh <tag> [no-profile|profile] [a|b|all]
+#   (part a: tests, two-group benches and the phase split; part b: single
+#   group and pipeline benches; all: both, the default)
 set -u
 export TMPDIR=/tmp
 tag=$1
@@ -22,6 +24,8 @@ step() {  # step <name> <seconds> <command...>
   grep '^{' $O/$name.log | tail -1 | cut -c1-400
   if [ $rc -ne 0 ]; then echo "[$name] rc=$rc: stop"; tail -20 $O/$name.log; exit $rc; fi
 }
+part=${3:-all}
+if [ "$part" != "b" ]; then
 step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
 tail -2 $O/tests.log
 step bench_c3 600 python bench.py
@@ -36,19 +40,22 @@ if [ -f $TUNE ] && [ "$(cat $(dirname $TUNE)/source_hash 2>/dev/null)" != "$SRC"
 elif [ -f $TUNE ]; then
   step phases_c3_shard0of8 300 env HYG_LIB_PATH=$TUNE HYG_DEBUG_PHASES=1 python bench.py --shard 0/8 --no-cpu-baseline --steps 1 --warmup 0
 fi
+fi
+if [ "$part" != "a" ]; then
 step bench_c2 600 python tools/bench_sg.py
 step bench_c1 600 python tools/bench_sg.py --config c1
 step bench_pipe 600 python tools/bench_pipeline.py
 step bench_pipe_concurrent 600 python tools/bench_pipeline.py --concurrent 8,16
+fi
 rc=0
-if [ "${2:-}" != "no-profile" ]; then  # (the profile set can run as its own call: bash tools/gpu_profile.sh <tag>)
+if [ "${2:-}" != "no-profile" ] && [ "$part" = "all" ]; then  # (the profile set can run as its own call: bash tools/gpu_profile.sh <tag>)
   bash tools/gpu_profile.sh $tag > $O/profile.log 2>&1; rc=$?
   tail -5 $O/profile.log
 fi
 mkdir -p $O/out
 for n in bench_c3 bench_c4 bench_c5 bench_c3_shard0of8 bench_c4_shard0of8 bench_c2 bench_c1 bench_pipe bench_pipe_concurrent; do
-  grep '^{' $O/$n.log | tail -1 > $O/out/${tag}_$n.json
+  [ -f $O/$n.log ] && grep '^{' $O/$n.log | tail -1 > $O/out/${tag}_$n.json
 done
-grep -h "phases" $O/phases_c3_shard0of8.log > $O/out/${tag}_phases_c3_shard0of8.log 2>/dev/null
+[ -f $O/phases_c3_shard0of8.log ] && grep -h "phases" $O/phases_c3_shard0of8.log > $O/out/${tag}_phases_c3_shard0of8.log
 cp $O/host.txt $O/out/${tag}_host.txt
 exit $rc
