@@ -1097,7 +1097,36 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       }
       lds_barrier();
       if (!PE) { SG_PH(16); }
-      const double ea = (va > HYG_NINF) ? hyg_exp(va - Amax[vr]) : 0.0;
+      double ea;
+      if (SPLIT && wv == NT / 64) {
+        // the G wave (threads NT .. NT + K^2 form G[r][q], below otherwise): its
+        // e_n and G exps in one straight-line block, so the two chains interleave
+        const int gi = tid - NT;  // (r, q) = (gi / K, gi % K)
+        const bool gth = gi < K * K;
+        const int r = gth ? gi / K : 0, q = gth ? gi - (gi / K) * K : 0;
+        double m = HYG_NINF;
+#pragma unroll
+        for (int rr = 0; rr < K; ++rr) m = dmax(m, Amax[rr] + logP[rr * K + q]);
+        const double xg = (Amax[r] + logP[r * K + q]) - m;
+        const double xa = (va > HYG_NINF) ? va - Amax[vr] : 0.0;
+        const double eg = hyg_exp(xg), e1 = hyg_exp(xa);
+        ea = (va > HYG_NINF) ? e1 : 0.0;
+        if (gth) {
+          Gq[gi] = (m > HYG_NINF) ? eg : 0.0;
+          if (r == 0) mqv[q] = m;
+        }
+      } else {
+        ea = (va > HYG_NINF) ? hyg_exp(va - Amax[vr]) : 0.0;
+        const int gi = tid;  // 256 threads: (r, q) = (gi / K, gi % K)
+        if (!SPLIT && gi < K * K) {
+          const int r = gi / K, q = gi - (gi / K) * K;
+          double m = HYG_NINF;
+#pragma unroll
+          for (int rr = 0; rr < K; ++rr) m = dmax(m, Amax[rr] + logP[rr * K + q]);
+          Gq[gi] = (m > HYG_NINF) ? hyg_exp((Amax[r] + logP[r * K + q]) - m) : 0.0;
+          if (r == 0) mqv[q] = m;
+        }
+      }
       if (tid < NT && va > HYG_NINF) {
         const hyg_u128 im = hyg_fix100(ea);  // < 2^101: limbs of 34, 34 and 33 bits
         unsigned long long* el = Elimb + 3 * vr;
@@ -1106,17 +1135,6 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         __hip_atomic_fetch_add(el + 1, ((im.lo >> 34) | (im.hi << 30)) & kL, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(el + 2, im.hi >> 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      {
-        const int gi = SPLIT ? tid - NT : tid;  // (r, q) = (gi / K, gi % K)
-        if (gi >= 0 && gi < K * K) {
-          const int r = gi / K, q = gi - (gi / K) * K;
-          double m = HYG_NINF;
-#pragma unroll
-          for (int rr = 0; rr < K; ++rr) m = dmax(m, Amax[rr] + logP[rr * K + q]);
-          Gq[gi] = (m > HYG_NINF) ? hyg_exp((Amax[r] + logP[r * K + q]) - m) : 0.0;
-          if (r == 0) mqv[q] = m;
-        }
       }
       if (!PE) { SG_PH(17); }
       lds_barrier();
