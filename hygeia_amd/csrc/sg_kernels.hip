@@ -596,7 +596,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
   double* redc = (double*)(red + sg_red_w(NW));   // continuing particles: block max partials
   int* redn = (int*)(redc + NW);                  //   and finite counts (see the normalisation)
   double* Amax = (double*)(redn + NW + (NW & 1)); // [K] A_r (backward kernels)
-  unsigned long long* Elimb = (unsigned long long*)(Amax + K);  // [K][3] 34-bit limbs of E_r
+  unsigned long long* Elimb = (unsigned long long*)(Amax + K);  // [K][2] 51-bit limbs of E_r ([K][3] reserved)
   double* Gq = (double*)(Elimb + 3 * K);          // [K][K] G[r][q]
   double* mqv = Gq + K * K;                       // [K] m_q
   double* lsev = (double*)(smem + lay.lsev);
@@ -994,7 +994,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       // were behind the previous step's last barrier; block reductions do not
       // touch them)
       if (tid < K) Amax[tid] = HYG_NINF;
-      if (tid < 3 * K) Elimb[tid] = 0ull;
+      if (tid < 2 * K) Elimb[tid] = 0ull;
       lds_barrier();
       if (check_top) {
         // every value loaded first (one LDS round trip), then a branch-free test
@@ -1128,13 +1128,13 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         }
       }
       if (tid < NT && va > HYG_NINF) {
-        const hyg_u128 im = hyg_fix100(ea);  // < 2^101: limbs of 34, 34 and 33 bits
-        unsigned long long* el = Elimb + 3 * vr;
-        constexpr unsigned long long kL = (1ull << 34) - 1;
+        // e_n <= 1, so the image is <= 2^100: limbs of 51 and 50 bits, whose sums
+        // over <= 256 particles stay below 2^59 (two LDS adds per particle)
+        const hyg_u128 im = hyg_fix100(ea);
+        unsigned long long* el = Elimb + 2 * vr;
+        constexpr unsigned long long kL = (1ull << 51) - 1;
         __hip_atomic_fetch_add(el + 0, im.lo & kL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(el + 1, ((im.lo >> 34) | (im.hi << 30)) & kL, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(el + 2, im.hi >> 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(el + 1, (im.lo >> 51) | (im.hi << 13), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (!PE) { SG_PH(17); }
       lds_barrier();
@@ -1145,13 +1145,11 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         // LDS round trip per term), in r order as before (the same FMA chain)
         double Er = 0.0;
         if (lane < K) {
-          const unsigned long long* el = Elimb + 3 * lane;
-          // E_r = l0 + l1 2^34 + l2 2^68 (each limb a sum of <= 256 values below 2^34)
+          const unsigned long long* el = Elimb + 2 * lane;
+          // E_r = l0 + l1 2^51 (l0 < 2^59, l1 < 2^58: sums of <= 256 limbs)
           hyg_u128 e, x;
           e.lo = el[0]; e.hi = 0;
-          x.lo = el[1] << 34; x.hi = el[1] >> 30;
-          e = hyg_u128_add(e, x);
-          x.lo = 0; x.hi = el[2] << 4;
+          x.lo = el[1] << 51; x.hi = el[1] >> 13;
           e = hyg_u128_add(e, x);
           Er = hyg_u128_to_f64(e, 100);
         }
