@@ -233,6 +233,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--history-gib", type=float, default=100.0, help="forward->backward history budget in HBM")
     ap.add_argument("--launch-chains", type=int, default=768, help="chains per launch when over the budget")
+    ap.add_argument("--no-batch-merge", action="store_true",
+                    help="A/B: keep a partial last launch of --launch-chains chains on its own")
+    ap.add_argument("--no-tail-overlap", action="store_true",
+                    help="A/B: no tail overlap in the launch (hyg_tg_set_tail_overlap(0))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", default=None, metavar="R/W",
                     help="run only rank R's chains of a W-rank job on this one GPU (a projection of one rank of "
@@ -263,6 +267,8 @@ def main():
     from hygeia_amd import _lib, parallel, synthetic, two_group
 
     L = _lib.load()
+    if args.no_tail_overlap:
+        _lib.check(L.hyg_tg_set_tail_overlap(0))
     K, M, B = args.K, args.M, args.B
     # ---- synthetic workload, resident in HBM (every rank holds the genome's counts)
     data = synthetic.simulate_device(args.sites, args.samples, args.samples, K=K, coverage=args.coverage,
@@ -285,9 +291,17 @@ def main():
     # launches: all chains at once while the forward->backward history fits the
     # budget, else batches of --launch-chains (one full round of resident
     # workgroups each) sharing one history buffer, run back to back
+    budget = args.history_gib * 2 ** 30
     batches = [chains]
-    if two_group.DeviceChains.workspace_bytes(model, chains) > args.history_gib * 2 ** 30:
+    if two_group.DeviceChains.workspace_bytes(model, chains) > budget:
         batches = [chains[i:i + args.launch_chains] for i in range(0, len(chains), args.launch_chains)]
+        # a partial last batch (the 1-GPU C4 job: 3 x 768 + 24 of its shortest
+        # chains) joins the one before when the history still fits: its chains
+        # start in the slots that batch's shorter chains free, instead of a
+        # launch of its own at low occupancy
+        if (not args.no_batch_merge and len(batches) > 1 and len(batches[-1]) < args.launch_chains
+                and two_group.DeviceChains.workspace_bytes(model, batches[-2] + batches[-1]) <= budget):
+            batches[-2:] = [batches[-2] + batches[-1]]
     ws = torch.empty(max(two_group.DeviceChains.workspace_bytes(model, b) for b in batches), dtype=torch.uint8,
                      device=dev)
     seg_of = {(ci << 32) | b: (s0, r0, rl) for (ci, b, s0, n, r0, rl) in segs}

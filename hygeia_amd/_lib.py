@@ -113,7 +113,7 @@ class SgChain(C.Structure):
 
 
 EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy", "hyg_tg_num_particles",
-           "hyg_tg_threads_per_chain", "hyg_tg_force_threads", "hyg_sg_force_key_drop", "hyg_tg_chains_per_cu", "hyg_tg_lds_bytes",
+           "hyg_tg_threads_per_chain", "hyg_tg_force_threads", "hyg_tg_set_tail_overlap", "hyg_sg_force_key_drop", "hyg_tg_chains_per_cu", "hyg_tg_lds_bytes",
            "hyg_tg_emission", "hyg_tg_workspace_bytes", "hyg_tg_run_chains", "hyg_tg_run_chain_host",
            "hyg_tg_run_chains_host",
            "hyg_device_count", "hyg_device_slot_acquire", "hyg_device_slot_release", "hyg_set_device",
@@ -182,6 +182,8 @@ def load(import_torch: bool = True) -> C.CDLL:
     L.hyg_tg_threads_per_chain.argtypes = [vp, i32]
     L.hyg_tg_force_threads.restype = C.c_int
     L.hyg_tg_force_threads.argtypes = [i32, i32]
+    L.hyg_tg_set_tail_overlap.restype = C.c_int
+    L.hyg_tg_set_tail_overlap.argtypes = [i32]
     L.hyg_sg_force_key_drop.restype = C.c_int
     L.hyg_sg_force_key_drop.argtypes = [i32]
     L.hyg_tg_chains_per_cu.restype = i32

@@ -380,6 +380,11 @@ int hyg_tg_force_threads(int32_t forward, int32_t backward) {
   return rc == HYG_OK ? rc : fail(rc, "unsupported workgroup size");
 }
 
+int hyg_tg_set_tail_overlap(int32_t on) {
+  hyg::tg_set_tail_overlap(on != 0);
+  return HYG_OK;
+}
+
 int hyg_sg_force_key_drop(int32_t bits) {
   const int rc = hyg::sg_force_key_drop(bits);
   return rc == HYG_OK ? rc : fail(rc, "key bits out of range [8, 60]");

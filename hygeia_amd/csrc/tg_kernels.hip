@@ -2872,7 +2872,7 @@ BwdFn bwd_kernel(const hyg_tg_consts& c) {
 
 template <int NT>
 static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
-                            const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
+                            const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s, bool timed) {
   Lay lf = make_layout(c.K, c.M, c.B, c.Nmax, NT, false);
   if (lf.total > 160 * 1024) return HYG_EUNSUPPORTED;
   static const char* rv = tuning_env("HYG_TOPSET_R");  // tuning: 1 (A <= 64 per wave) or 2
@@ -2885,10 +2885,10 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
   const bool want_dbg = has_phases<NT>() && want_phases();
   if (want_dbg) (void)hipMalloc((void**)&dbg, sizeof(unsigned long long) * kPh * n_chains);
   if (dbg) (void)hipMemsetAsync(dbg, 0, sizeof(unsigned long long) * kPh * n_chains, s);
-  ev_record(1, false, s);
+  if (timed) ev_record(1, false, s);
   hipLaunchKernelGGL(fwd_kernel<NT>(c), dim3(n_chains), dim3(NT), lf.total, s, md, chains_dev, E, ws,
                      out.status, out.log_z, out.final_log_weights, lf, dbg);
-  ev_record(1, true, s);
+  if (timed) ev_record(1, true, s);
   if (hipGetLastError() != hipSuccess) return HYG_EDEVICE;
   if (dbg) {
     std::vector<unsigned long long> h((size_t)kPh * n_chains);
@@ -2927,7 +2927,7 @@ static int launch_forward_nt(const ModelDev& md, const hyg_tg_consts& c, const C
 
 template <int NT>
 static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
-                              const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s) {
+                              const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s, bool timed) {
   const Lay lb = make_layout(c.K, c.M, c.B, c.Nmax, NT, true, bwd_gw(c, NT));
   if (lb.total > 160 * 1024) return HYG_EUNSUPPORTED;
   if (c.M > NT) return HYG_EUNSUPPORTED;  // one ancestor per thread in the record read-ahead
@@ -2938,11 +2938,11 @@ static int launch_backward_nt(const ModelDev& md, const hyg_tg_consts& c, const 
   unsigned long long* dbgb = nullptr;
   if (want_dbg) (void)hipMalloc((void**)&dbgb, sizeof(unsigned long long) * kPh * n_chains);
   if (dbgb) (void)hipMemsetAsync(dbgb, 0, sizeof(unsigned long long) * kPh * n_chains, s);
-  ev_record(2, false, s);
+  if (timed) ev_record(2, false, s);
   hipLaunchKernelGGL(bwd_kernel<NT>(c), dim3(n_chains), dim3(NT), lb.total, s, md, chains_dev, E,
                      (const uint8_t*)ws, (const int32_t*)out.status, out.merged, out.control, out.kase,
                      out.split_probs, out.regime_probs, out.status, lb, dbgb, ws);
-  ev_record(2, true, s);
+  if (timed) ev_record(2, true, s);
   if (dbgb) {
     std::vector<unsigned long long> h((size_t)kPh * n_chains);
     (void)hipStreamSynchronize(s);
@@ -2987,26 +2987,119 @@ int tg_resident_per_cu(const hyg_tg_consts& c, int n_chains) {
   }
 }
 
+static int launch_forward(int nt, const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev,
+                          int n_chains, const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s,
+                          bool timed) {
+  switch (nt) {
+    case 64: return launch_forward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+    case 128: return launch_forward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+    case 256: return launch_forward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+    case 768: return launch_forward_nt<768>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+    default: return launch_forward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+  }
+}
+static int launch_backward(int nt, const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev,
+                           int n_chains, const double* E, uint8_t* ws, const hyg_tg_outputs& out, hipStream_t s,
+                           bool timed) {
+  switch (nt) {
+    case 64: return launch_backward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+    case 128: return launch_backward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+    case 256: return launch_backward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+    case 768: return launch_backward_nt<768>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+    default: return launch_backward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s, timed);
+  }
+}
+
+// One wave that sleeps about 0.1 ms (32 x s_sleep 127, ~8 k cycles each). It
+// sits between the head's forward and its backward on the second stream so that
+// the tail's forward, released by the same event on the launch stream, takes its
+// CUs before the backward's workgroups fill them (see launch_chains).
+__global__ void tg_dispatch_guard_kernel() {
+  for (int i = 0; i < 32; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+namespace {
+// The per-chain outputs of chains [c0, ...) of a launch; the per-site outputs
+// are addressed through each chain's out_begin and need no offset.
+hyg_tg_outputs outputs_from(const hyg_tg_outputs& o, const hyg_tg_consts& c, int c0) {
+  hyg_tg_outputs r = o;
+  r.status = o.status + c0;
+  r.log_z = o.log_z + c0;
+  if (o.final_log_weights) r.final_log_weights = o.final_log_weights + (size_t)c0 * c.Nmax;
+  return r;
+}
+// The second stream and two events of a device for the tail overlap
+// (created on first use, kept for the process).
+struct TailAux {
+  hipStream_t s = nullptr;
+  hipEvent_t head_done = nullptr, bwd_done = nullptr;
+  bool ok = false, tried = false;
+};
+TailAux* tail_aux() {
+  static TailAux aux[32];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return nullptr;
+  TailAux& a = aux[dev];
+  if (!a.tried) {
+    a.tried = true;
+    a.ok = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&a.head_done, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&a.bwd_done, hipEventDisableTiming) == hipSuccess;
+  }
+  return a.ok ? &a : nullptr;
+}
+bool g_tail_overlap = true;  // hyg_tg_set_tail_overlap
+}  // namespace
+
+void tg_set_tail_overlap(bool on) { g_tail_overlap = on; }
+
+// The whole launch: forward of every chain, then the backward of every chain.
+//
+// Tail overlap. When the forward's LDS holds one chain per CU (the C5 shape)
+// and the chains fill more than one round of CUs with a partial last round, the
+// last round leaves most CUs idle for a full chain's latency (C5: 1 164 chains
+// = four rounds of 256 and a fifth of 140, 52 of them full length). The
+// launch is then split: the forward of the full rounds (the head, the first
+// chains in launch order) and of the rest (the tail) run back to back on the
+// launch stream, and the head's backward runs on a second stream as soon as
+// the head's forward is done, on the CUs the tail's forward leaves free; the
+// tail's backward follows its forward. Each chain's forward still precedes its
+// backward, no chain's buffers are shared, and the widths are those of the
+// whole launch, so the outputs are those of the unsplit launch (GPU test).
 int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* chains_dev, int n_chains,
                   const double* E, uint8_t* ws, const hyg_tg_outputs& out, void* stream) {
   if (n_chains <= 0) return HYG_OK;
   hipStream_t s = (hipStream_t)stream;
-  int rc;
-  switch (threads_per_chain(false, c, n_chains)) {
-    case 64: rc = launch_forward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s); break;
-    case 128: rc = launch_forward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s); break;
-    case 256: rc = launch_forward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s); break;
-    case 768: rc = launch_forward_nt<768>(md, c, chains_dev, n_chains, E, ws, out, s); break;
-    default: rc = launch_forward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s); break;
+  const int ntf = threads_per_chain(false, c, n_chains), ntb = threads_per_chain(true, c, n_chains);
+  int head = n_chains;
+  TailAux* aux = nullptr;
+  if (g_tail_overlap && n_chains > device_cus() && n_chains % device_cus() != 0 &&
+      tg_resident_per_cu(c, n_chains) == 1 && (aux = tail_aux()) != nullptr)
+    head = n_chains - n_chains % device_cus();
+  if (head == n_chains) {
+    const int rc = launch_forward(ntf, md, c, chains_dev, n_chains, E, ws, out, s, true);
+    if (rc != HYG_OK) return rc;
+    return launch_backward(ntb, md, c, chains_dev, n_chains, E, ws, out, s, true);
   }
+  const int tail = n_chains - head;
+  const hyg_tg_outputs out_t = outputs_from(out, c, head);
+  ev_record(1, false, s);
+  int rc = launch_forward(ntf, md, c, chains_dev, head, E, ws, out, s, false);
   if (rc != HYG_OK) return rc;
-  switch (threads_per_chain(true, c, n_chains)) {
-    case 64: return launch_backward_nt<64>(md, c, chains_dev, n_chains, E, ws, out, s);
-    case 128: return launch_backward_nt<128>(md, c, chains_dev, n_chains, E, ws, out, s);
-    case 256: return launch_backward_nt<256>(md, c, chains_dev, n_chains, E, ws, out, s);
-    case 768: return launch_backward_nt<768>(md, c, chains_dev, n_chains, E, ws, out, s);
-    default: return launch_backward_nt<512>(md, c, chains_dev, n_chains, E, ws, out, s);
-  }
+  if (hipEventRecord(aux->head_done, s) != hipSuccess) return HYG_EDEVICE;
+  rc = launch_forward(ntf, md, c, chains_dev + head, tail, E, ws, out_t, s, false);
+  if (rc != HYG_OK) return rc;
+  ev_record(1, true, s);
+  if (hipStreamWaitEvent(aux->s, aux->head_done, 0) != hipSuccess) return HYG_EDEVICE;
+  hipLaunchKernelGGL(tg_dispatch_guard_kernel, dim3(1), dim3(64), 0, aux->s);
+  ev_record(2, false, aux->s);
+  rc = launch_backward(ntb, md, c, chains_dev, head, E, ws, out, aux->s, false);
+  if (rc != HYG_OK) return rc;
+  if (hipEventRecord(aux->bwd_done, aux->s) != hipSuccess) return HYG_EDEVICE;
+  rc = launch_backward(ntb, md, c, chains_dev + head, tail, E, ws, out_t, s, false);
+  if (rc != HYG_OK) return rc;
+  if (hipStreamWaitEvent(s, aux->bwd_done, 0) != hipSuccess) return HYG_EDEVICE;
+  ev_record(2, true, s);
+  return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }
-
 }  // namespace hyg

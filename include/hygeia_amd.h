@@ -135,6 +135,16 @@ size_t hyg_tg_lds_bytes(const hyg_tg_model* model, int32_t threads, int32_t back
  * on it: every width computes the same bits. */
 int hyg_tg_force_threads(int32_t forward, int32_t backward);
 
+/* Tail overlap of hyg_tg_run_chains (on = 1, the default; 0 = off) for every
+ * later launch in the process. When the forward holds one chain per CU and
+ * the chains fill more than one round of CUs with a partial last round (the
+ * K = 12 stress shape: 1 164 chains on 256 CUs), the launch runs the forward
+ * of the full rounds, then the rest's forward on the launch stream while the
+ * full rounds' backward runs on a second stream of the library's, on the CUs
+ * the last round leaves idle; the call's stream waits for both. The results
+ * do not depend on it (GPU test). Not thread-safe. No reference counterpart. */
+int hyg_tg_set_tail_overlap(int32_t on);
+
 /* Test override of the single-group chain's log-weight sort for every later
  * launch in the process. The sort orders one 64-bit word per particle: the
  * order key's top 64 - bits bits and the particle index (bits = 8, or 0 for

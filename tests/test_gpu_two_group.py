@@ -387,3 +387,48 @@ def test_infer_many_equals_single_task_runs(tmp_path):
                 assert gzip.open(a).read() == gzip.open(b).read(), nm
             else:  # the flags files name their own --results_dir
                 assert a.read_text().replace(str(one), "R") == b.read_text().replace(str(many), "R"), nm
+
+
+def test_tail_overlap_equals_one_launch(oracle):
+    """The tail overlap of hyg_tg_run_chains (the C5 shape, one forward chain
+    per CU: more chains than CUs with a partial last round run as the full
+    rounds' forward, then the rest's forward beside the full rounds' backward on
+    a second stream) gives the outputs of the unsplit launch, and chains on
+    either side of the split equal their own oracle runs."""
+    from hygeia_amd import _lib, two_group
+
+    L = _lib.load()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    K, M, B, S = 12, 50, 25, 3
+    mu, sg, theta, d, p = _setup(oracle, K, M, B, 1600, S, 100.0, 35)
+    obs = {"control": d["meth_control"], "case": d["meth_case"]}
+    tot = {"control": d["tot_control"], "case": d["tot_case"]}
+    n_chains = cus + 37
+    rng = np.random.default_rng(5)
+    chains, out = [], 0
+    for i in range(n_chains):
+        n = int(rng.integers(20, 90)) if i < cus else int(rng.integers(1, 120))
+        s0 = int(rng.integers(0, 1600 - n))
+        chains.append((s0, n, i % 3, 7000 + i, out))
+        out += n
+    model = _model(mu, sg, theta, M, B, int(max(d["tot_control"].max(), d["tot_case"].max())), 200)
+    assert L.hyg_tg_chains_per_cu(model.handle, n_chains) == 1  # the split applies
+    runs = []
+    for on in (1, 0):
+        _lib.check(L.hyg_tg_set_tail_overlap(on))
+        try:
+            runs.append(two_group.run_chains_host(obs, tot, model, chains, out, final_weights=True))
+        finally:
+            L.hyg_tg_set_tail_overlap(1)
+    a, b = runs
+    assert (a["status"] == 0).all()
+    for k in ("merged", "control", "case", "split_probs", "regime_probs", "log_z", "final_w", "status"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    E_ref = oracle.emission(p, d["meth_control"], d["tot_control"], d["meth_case"], d["tot_case"])
+    for i in (0, cus - 1, cus, n_chains - 1):
+        s0, n, seed, cid, o0 = chains[i]
+        ref = oracle.chain(p, E_ref[s0:s0 + n], seed, cid)
+        for k in ("merged", "control", "case", "split_probs", "regime_probs"):
+            np.testing.assert_array_equal(a[k][o0:o0 + n], ref[k], err_msg=f"chain {i} {k}")
+        assert a["log_z"][i] == ref["log_z"]
+        np.testing.assert_array_equal(a["final_w"][i], ref["final_log_weights"])
