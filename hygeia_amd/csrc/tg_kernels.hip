@@ -22,6 +22,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 #include "../../include/hyg_arith.h"
@@ -3031,6 +3032,7 @@ hyg_tg_outputs outputs_from(const hyg_tg_outputs& o, const hyg_tg_consts& c, int
 // The second stream and two events of a device for the tail overlap
 // (created on first use, kept for the process).
 struct TailAux {
+  std::mutex mu;  // one split launch enqueued at a time (the events are shared)
   hipStream_t s = nullptr;
   hipEvent_t head_done = nullptr, bwd_done = nullptr;
   bool ok = false, tried = false;
@@ -3040,6 +3042,8 @@ TailAux* tail_aux() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return nullptr;
   TailAux& a = aux[dev];
+  static std::mutex init_mu;
+  std::lock_guard<std::mutex> lock(init_mu);
   if (!a.tried) {
     a.tried = true;
     a.ok = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) == hipSuccess &&
@@ -3083,6 +3087,7 @@ int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* ch
   }
   const int tail = n_chains - head;
   const hyg_tg_outputs out_t = outputs_from(out, c, head);
+  std::lock_guard<std::mutex> lock(aux->mu);
   ev_record(1, false, s);
   int rc = launch_forward(ntf, md, c, chains_dev, head, E, ws, out, s, false);
   if (rc != HYG_OK) return rc;
