@@ -313,12 +313,11 @@ def main():
             rows += n
         dcb = two_group.DeviceChains(model, rebased, rows, device=dev, workspace=ws)
         # final gather (aggregate_results.py:71-206): per-site posterior counts over
-        # all trajectories of all seeds, summed over ranks by one all-reduce
-        src = np.concatenate([np.arange(c[4] + seg_of[c[3]][1], c[4] + seg_of[c[3]][1] + seg_of[c[3]][2])
-                              for c in rebased])
-        dst = np.concatenate([np.arange(seg_of[c[3]][0] + seg_of[c[3]][1], seg_of[c[3]][0] + seg_of[c[3]][1]
-                                        + seg_of[c[3]][2]) for c in rebased])
-        runs.append((dcb, torch.from_numpy(src).to(dev), torch.from_numpy(dst).to(dev)))
+        # all trajectories of all seeds (one HIP kernel over the chains' trimmed
+        # rows), summed over ranks by one all-reduce
+        # (one call per seed: a seed's chains cover disjoint sites, so no atomics)
+        tabs = [(torch.from_numpy(t).to(dev), int(t[:, 2].max())) for t in parallel.seed_tables(rebased, seg_of)]
+        runs.append((dcb, tabs, None))
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
     E = torch.empty((args.sites, 2 * K), dtype=torch.float64, device=dev)
@@ -329,15 +328,16 @@ def main():
         runs[0][0].emission(data["meth_control"], data["tot_control"], data["meth_case"], data["tot_case"], E=E,
                             stream=sp)
         ms3 = (ctypes.c_float * 3)()
-        for i, (dcb, rows_out, rows_site) in enumerate(runs):
+        for i, (dcb, _, _) in enumerate(runs):
             dcb.run(E, stream=sp)
             _lib.check(L.hyg_tg_last_kernel_ms(ms3))
             kms += np.array(list(ms3)) * np.array([1.0 if i == 0 else 0.0, 1.0, 1.0])
         with torch.cuda.stream(stream):
             counts.zero_()
-            for dcb, rows_out, rows_site in runs:
-                parallel.posterior_counts(dcb.split_probs, dcb.regime_probs, B, rows_out, rows_site, args.sites,
-                                          counts)
+            for dcb, tabs, _ in runs:
+                for tab, max_rows in tabs:
+                    parallel.posterior_counts_device(L, dcb.split_probs, dcb.regime_probs, B, tab, max_rows, counts,
+                                                     sp, exclusive=True)
             parallel.allreduce_counts(counts)
         return kms
 

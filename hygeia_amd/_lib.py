@@ -122,7 +122,7 @@ EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy
            "hyg_sg_workspace_bytes", "hyg_sg_run_chains", "hyg_sg_run_chain_host",
            "hyg_sg_pe_params_default", "hyg_sg_pe_theta_rows", "hyg_sg_pe_workspace_bytes", "hyg_sg_run_chains_pe",
            "hyg_sg_run_chain_host_pe", "hyg_bed_labels", "hyg_bed_format", "hyg_pre_collapse",
-           "hyg_dmp_site_counts", "hyg_dmp_fdr", "hyg_dmp_weighted_fdr")
+           "hyg_dmp_site_counts", "hyg_dmp_fdr", "hyg_dmp_weighted_fdr", "hyg_tg_posterior_counts")
 
 
 class DmpGroup(C.Structure):
@@ -249,6 +249,8 @@ def load(import_torch: bool = True) -> C.CDLL:
                                  vp, i64]
     L.hyg_sg_run_chain_host_pe.restype = C.c_int
     L.hyg_sg_run_chain_host_pe.argtypes = [vp, C.POINTER(SgPeParams), vp, vp, i32, i32, u64, u64, vp, vp]
+    L.hyg_tg_posterior_counts.restype = C.c_int
+    L.hyg_tg_posterior_counts.argtypes = [vp, vp, i32, i32, vp, i32, i64, i32, vp, vp]
     L.hyg_dmp_site_counts.restype = C.c_int
     L.hyg_dmp_site_counts.argtypes = [vp, vp, vp, i32, i32, C.POINTER(DmpGroup), C.POINTER(i64), i32, i32, i64, vp,
                                       vp, vp]

@@ -1002,6 +1002,18 @@ struct SortedStats {
 
 extern "C" {
 
+int hyg_tg_posterior_counts(const float* split, const float* regime, int32_t K, int32_t B, const int64_t* segments,
+                            int32_t n_segments, int64_t max_rows, int32_t exclusive, int32_t* counts,
+                            void* stream) {
+  if (!split || !regime || !counts || (n_segments > 0 && !segments) || K < 1 || K > HYG_KMAX || B < 1 ||
+      n_segments < 0 || max_rows < 0)
+    return fail(HYG_EINVAL, "hyg_tg_posterior_counts: invalid arguments");
+  if (!have_device()) return fail(HYG_EDEVICE, "no HIP device: hygeia_amd has no CPU fallback");
+  if (launch_post_counts(split, regime, 2 * K, B, segments, n_segments, max_rows, exclusive != 0, counts, stream))
+    return fail(HYG_EDEVICE, "posterior_counts launch failed");
+  return HYG_OK;
+}
+
 int hyg_dmp_site_counts(const int16_t* merged, const int16_t* control, const int16_t* kase, int32_t B, int32_t K,
                         const hyg_dmp_group* groups, const int64_t* block_rows, int32_t n_groups, int32_t n_seeds,
                         int64_t n_sites, int32_t* counts, int32_t* pairs, void* stream) {

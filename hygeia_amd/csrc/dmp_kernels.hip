@@ -88,6 +88,36 @@ dmp_site_counts_kernel(const int16_t* __restrict__ merged, const int16_t* __rest
   }
 }
 
+// ------------------------------------------------- posterior counts
+// The job's gather of hyg_tg_run_chains outputs (bench.py, parallel.py):
+// counts[site][0] += rint(B split[row]), counts[site][1 + j] += rint(B regime[row][j])
+// over every trimmed row of every segment (out_row, site, n). The probabilities
+// are means over the B trajectories, so B p is an integer in f64; rint is
+// torch.round's half-to-even. One thread per count element of a segment's
+// contiguous [site0 (1 + 2K), (site0 + n)(1 + 2K)) range (coalesced), grid-
+// strided in x, blockIdx.y = segment. EXCL: the call's segments cover disjoint
+// sites (the caller's guarantee: one seed's chains), so a plain read-add-write;
+// otherwise integer atomics (order-free, but each a read-modify-write beyond L2:
+// about 10x slower at the C3 size).
+template <bool EXCL>
+__global__ void __launch_bounds__(256)
+post_counts_kernel(const float* __restrict__ split, const float* __restrict__ regime, int K2, double Bd,
+                   const int64_t* __restrict__ seg, int32_t* __restrict__ counts) {
+  const int64_t row0 = seg[3 * (int64_t)blockIdx.y], site0 = seg[3 * (int64_t)blockIdx.y + 1],
+                n = seg[3 * (int64_t)blockIdx.y + 2];
+  const int C = 1 + K2;
+  const int64_t ne = n * C;
+  int32_t* __restrict__ out = counts + site0 * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / C;
+    const int c = (int)(e - i * C);
+    const float p = (c == 0) ? split[row0 + i] : regime[(row0 + i) * K2 + (c - 1)];
+    const int32_t v = (int32_t)rint((double)p * Bd);
+    if constexpr (EXCL) out[e] += v;
+    else atomicAdd(out + e, v);
+  }
+}
+
 // ------------------------------------------------------- FDR histogram
 __global__ void __launch_bounds__(256)
 dmp_hist_kernel(const int32_t* __restrict__ counts, int stride, int col, int64_t n, int P,
@@ -254,6 +284,20 @@ int launch_dmp_site_counts(const int16_t* merged, const int16_t* control, const 
     hipLaunchKernelGGL(dmp_site_counts_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        merged, control, kase, B, K, grp_row0, grp_site, blk_row, n_groups, n_seeds, n_rows_total,
                        counts, pairs);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_post_counts(const float* split, const float* regime, int K2, int B, const int64_t* seg, int n_seg,
+                       int64_t max_rows, int exclusive, int32_t* counts, void* stream) {
+  if (n_seg <= 0 || max_rows <= 0) return 0;
+  int64_t bx = (max_rows * (1 + K2) + 255) / 256;
+  if (bx > 256) bx = 256;  // elements grid-strided: up to 256 x 256 threads per segment
+  if (exclusive)
+    hipLaunchKernelGGL(post_counts_kernel<true>, dim3((unsigned)bx, (unsigned)n_seg), dim3(256), 0,
+                       (hipStream_t)stream, split, regime, K2, (double)B, seg, counts);
+  else
+    hipLaunchKernelGGL(post_counts_kernel<false>, dim3((unsigned)bx, (unsigned)n_seg), dim3(256), 0,
+                       (hipStream_t)stream, split, regime, K2, (double)B, seg, counts);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -62,6 +62,41 @@ def posterior_counts(split_probs, regime_probs, B: int, rows_out, rows_site, n_s
     return counts
 
 
+def posterior_counts_device(L, split_probs, regime_probs, B: int, segments, max_rows: int, counts, stream=0,
+                            exclusive: bool = False):
+    """The same sum as posterior_counts on the device, in one HIP kernel
+    (hyg_tg_posterior_counts): segments is an int64 device tensor [n][3] of
+    (output row, site, rows) per chain, as segment_table builds it; exclusive:
+    the caller guarantees the segments cover disjoint sites (one seed's chains),
+    so no atomics. Asynchronous on `stream` (a HIP stream handle; 0 = the null
+    stream)."""
+    from . import _lib
+
+    K = regime_probs.shape[1] // 2
+    _lib.check(L.hyg_tg_posterior_counts(split_probs.data_ptr(), regime_probs.data_ptr(), K, B,
+                                         segments.data_ptr(), int(segments.shape[0]), int(max_rows),
+                                         1 if exclusive else 0, counts.data_ptr(), stream))
+    return counts
+
+
+def seed_tables(chains, seg_of) -> List[np.ndarray]:
+    """segment_table of each seed's chains (each covers disjoint sites), in seed
+    order."""
+    seeds = sorted({c[2] for c in chains})
+    return [segment_table([c for c in chains if c[2] == sd], seg_of) for sd in seeds]
+
+
+def segment_table(chains, seg_of) -> np.ndarray:
+    """int64 [n][3] (output row, site, rows) of the trimmed rows of each chain
+    (site_begin, n_sites, seed, chain_id, out_begin); seg_of maps a chain id to
+    its segment's (site_begin, trim offset, trimmed rows)."""
+    t = np.empty((len(chains), 3), np.int64)
+    for i, c in enumerate(chains):
+        s0, r0, rl = seg_of[c[3]]
+        t[i] = (c[4] + r0, s0 + r0, rl)
+    return t
+
+
 def allreduce_counts(counts, always: bool = False):
     """Sum of the per-site counts over all ranks (in place); a no-op without an
     initialised process group, and at world size 1 unless `always` (which runs

@@ -341,6 +341,27 @@ int hyg_sg_run_chain_host_pe(const hyg_sg_model* model, const hyg_sg_pe_params* 
  *   multiple_testing.py:3-22     FDR_procedure, weighted_FDR_procedure
  * on trajectories resident in HBM (the outputs of hyg_tg_run_chains). */
 
+/* The job's gather of per-site posterior counts over trajectories and seeds
+ * (what aggregate_results.py:129,181 averages; bench.py's step ends with it):
+ * for every segment (out_row, site, n_rows) of the device array segments
+ * [n_segments][3] int64 and every i < n_rows,
+ *   counts[site + i][0]     += round(B * split[out_row + i])
+ *   counts[site + i][1 + j] += round(B * regime[out_row + i][j]),  j < 2K,
+ * round half to even (torch.round). split / regime are hyg_tg_outputs'
+ * split_probs / regime_probs, means over the B trajectories, so B p is an
+ * integer. counts [n_sites][1 + 2K] int32 (device) is added to, not cleared.
+ * exclusive = 1: the caller guarantees that the call's segments cover disjoint
+ * sites (e.g. the chains of one seed), and each count is a plain read-add-write
+ * (coalesced; the C3 job's 56 M rows in about 2 ms per seed); exclusive = 0:
+ * segments may share sites (several seeds in one call) and every add is an
+ * integer atomic (the same sums, about 22 ms for the C3 job). The caller keeps
+ * every row and site in range; max_rows (>= every n_rows) sizes the grid.
+ * Asynchronous on stream. Replaces a torch gather / round / index_add chain
+ * (parallel.posterior_counts, kept as the tests' reference). */
+int hyg_tg_posterior_counts(const float* split, const float* regime, int32_t K, int32_t B,
+                            const int64_t* segments, int32_t n_segments, int64_t max_rows, int32_t exclusive,
+                            int32_t* counts, void* stream);
+
 /* One chromosome segment: the same reported (trimmed) rows in every seed's
  * trajectory block. */
 typedef struct hyg_dmp_group {

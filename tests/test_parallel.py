@@ -112,3 +112,25 @@ def test_two_rank_reduce_equals_single_process(oracle):
     # two seeds x B trajectories per site, every site counted once per trajectory
     assert np.all(got[:, 1:1 + K].sum(1) == 2 * B)
     assert np.all(got[:, 1 + K:].sum(1) == 2 * B)
+
+
+def test_segment_table_matches_row_lists():
+    """parallel.segment_table (the device gather's chain table) expands to the
+    (output row, site) pairs the torch reference's index lists hold."""
+    from hygeia_amd import synthetic
+
+    segs = synthetic.segment_chains(synthetic.chromosome_sizes(900_000))
+    seg_of = {(ci << 32) | b: (s0, r0, rl) for (ci, b, s0, n, r0, rl) in segs}
+    chains, out = [], 0
+    for sd in (0, 1):
+        for (ci, b, s0, n, r0, rl) in segs:
+            chains.append((s0, n, sd, (ci << 32) | b, out))
+            out += n
+    tab = parallel.segment_table(chains, seg_of)
+    src = np.concatenate([np.arange(c[4] + seg_of[c[3]][1], c[4] + seg_of[c[3]][1] + seg_of[c[3]][2]) for c in chains])
+    dst = np.concatenate([np.arange(seg_of[c[3]][0] + seg_of[c[3]][1], seg_of[c[3]][0] + seg_of[c[3]][1]
+                                    + seg_of[c[3]][2]) for c in chains])
+    np.testing.assert_array_equal(np.concatenate([np.arange(a, a + n) for a, _, n in tab]), src)
+    np.testing.assert_array_equal(np.concatenate([np.arange(s, s + n) for _, s, n in tab]), dst)
+    # every site once per seed
+    assert np.bincount(dst, minlength=900_000).tolist() == [2] * 900_000
