@@ -6,9 +6,10 @@
 #   rocprofv3 profile set of the default workload (tools/gpu_profile.sh).
 # Outputs: gpurun_out/<tag>/* (only gpurun_out/ comes back from the box; copy
 # gpurun_out/<tag>/out/* and gpurun_out/prof_<tag>/* into profiles/ afterwards).
-# usage: bash tools/gpu_final.sh <tag> [no-profile|profile] [a|b|all]
+# usage: bash tools/gpu_final.sh <tag> [no-profile|profile] [a|b|c|all]
 #   (part a: tests, two-group benches and the phase split; part b: single
-#   group and pipeline benches; all: both, the default)
+#   group and pipeline benches; part c: the 2- and 4-rank shares of C3 / C4;
+#   all: a and b, the default)
 set -u
 export TMPDIR=/tmp
 tag=$1
@@ -25,7 +26,7 @@ step() {  # step <name> <seconds> <command...>
   if [ $rc -ne 0 ]; then echo "[$name] rc=$rc: stop"; tail -20 $O/$name.log; exit $rc; fi
 }
 part=${3:-all}
-if [ "$part" != "b" ]; then
+if [ "$part" = "a" ] || [ "$part" = "all" ]; then
 step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
 tail -2 $O/tests.log
 step bench_c3 600 python bench.py
@@ -41,7 +42,12 @@ elif [ -f $TUNE ]; then
   step phases_c3_shard0of8 300 env HYG_LIB_PATH=$TUNE HYG_DEBUG_PHASES=1 python bench.py --shard 0/8 --no-cpu-baseline --steps 1 --warmup 0
 fi
 fi
-if [ "$part" != "a" ]; then
+if [ "$part" = "c" ]; then
+for j in c3 c4; do for w in 2 4; do
+  step bench_${j}_shard0of$w 300 python bench.py --job $j --shard 0/$w --no-cpu-baseline --steps 1
+done; done
+fi
+if [ "$part" != "a" ] && [ "$part" != "c" ]; then
 step bench_c2 600 python tools/bench_sg.py
 step bench_c1 600 python tools/bench_sg.py --config c1
 step bench_pipe 600 python tools/bench_pipeline.py
@@ -53,7 +59,7 @@ if [ "${2:-}" != "no-profile" ] && [ "$part" = "all" ]; then  # (the profile set
   tail -5 $O/profile.log
 fi
 mkdir -p $O/out
-for n in bench_c3 bench_c4 bench_c5 bench_c3_shard0of8 bench_c4_shard0of8 bench_c2 bench_c1 bench_pipe bench_pipe_concurrent; do
+for n in bench_c3 bench_c4 bench_c5 bench_c3_shard0of8 bench_c4_shard0of8 bench_c3_shard0of2 bench_c3_shard0of4 bench_c4_shard0of2 bench_c4_shard0of4 bench_c2 bench_c1 bench_pipe bench_pipe_concurrent; do
   [ -f $O/$n.log ] && grep '^{' $O/$n.log | tail -1 > $O/out/${tag}_$n.json
 done
 [ -f $O/phases_c3_shard0of8.log ] && grep -h "phases" $O/phases_c3_shard0of8.log > $O/out/${tag}_phases_c3_shard0of8.log
