@@ -317,7 +317,7 @@ def main():
         # rows), summed over ranks by one all-reduce
         # (one call per seed: a seed's chains cover disjoint sites, so no atomics)
         tabs = [(torch.from_numpy(t).to(dev), int(t[:, 2].max())) for t in parallel.seed_tables(rebased, seg_of)]
-        runs.append((dcb, tabs, None))
+        runs.append((dcb, tabs))
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
     E = torch.empty((args.sites, 2 * K), dtype=torch.float64, device=dev)
@@ -328,13 +328,13 @@ def main():
         runs[0][0].emission(data["meth_control"], data["tot_control"], data["meth_case"], data["tot_case"], E=E,
                             stream=sp)
         ms3 = (ctypes.c_float * 3)()
-        for i, (dcb, _, _) in enumerate(runs):
+        for i, (dcb, _) in enumerate(runs):
             dcb.run(E, stream=sp)
             _lib.check(L.hyg_tg_last_kernel_ms(ms3))
             kms += np.array(list(ms3)) * np.array([1.0 if i == 0 else 0.0, 1.0, 1.0])
         with torch.cuda.stream(stream):
             counts.zero_()
-            for dcb, tabs, _ in runs:
+            for dcb, tabs in runs:
                 for tab, max_rows in tabs:
                     parallel.posterior_counts_device(L, dcb.split_probs, dcb.regime_probs, B, tab, max_rows, counts,
                                                      sp, exclusive=True)
