@@ -474,6 +474,43 @@ __device__ __forceinline__ void block_scan128(hyg_u128 v, hyg_u128* out, unsigne
   out[threadIdx.x] = hyg_u128_add(pre, e2);
   if (threadIdx.x == 0) out[NT] = tot;
 }
+// The same scan with this thread's exclusive prefix and the block total
+// returned in registers: no LDS output, so a caller that needs only its own
+// prefix and the total needs no barrier behind it (red's readers are done when
+// it returns; its next writer must still be behind a barrier).
+template <int NT>
+__device__ __forceinline__ void block_scan128_regs(hyg_u128 v, unsigned char* red, hyg_u128* excl, hyg_u128* total) {
+  hyg_u128* r = (hyg_u128*)red;
+  const hyg_u128 inc = wave_incl128(v);
+  hyg_u128 wt;
+  wt.lo = rdlane64(inc.lo, 63); wt.hi = rdlane64(inc.hi, 63);
+  lds_barrier();
+  if (lane_id() == 0) r[wave_id()] = wt;
+  lds_barrier();
+  hyg_u128 pre = hyg_u128_zero(), tot = hyg_u128_zero();
+  if constexpr (NT / 64 <= HYG_SEQ_WAVES) {
+    for (int w = 0; w < NT / 64; ++w) {
+      if (w < wave_id()) pre = hyg_u128_add(pre, r[w]);
+      tot = hyg_u128_add(tot, r[w]);
+    }
+  } else {
+    const int l = lane_id(), wv = wave_id();
+    hyg_u128 x = hyg_u128_zero();
+    if (l < NT / 64) x = r[l];
+    x = wave_incl128(x);
+    tot.lo = rdlane64(x.lo, NT / 64 - 1);
+    tot.hi = rdlane64(x.hi, NT / 64 - 1);
+    if (wv > 0) {
+      pre.lo = rdlane64(x.lo, wv - 1);
+      pre.hi = rdlane64(x.hi, wv - 1);
+    }
+  }
+  hyg_u128 e2;  // inc - v
+  e2.lo = inc.lo - v.lo;
+  e2.hi = inc.hi - v.hi - (inc.lo < v.lo ? 1u : 0u);
+  *excl = hyg_u128_add(pre, e2);
+  *total = tot;
+}
 
 
 }  // namespace hyg

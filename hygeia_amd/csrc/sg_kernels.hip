@@ -823,17 +823,16 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
               logq[tid] = lq;
               sidx[tid] = idx;
             }
-            // reverse cumulative sums Q(k) = total - exclusive prefix (exact)
-            block_scan128<NB>(mq, cum, red);
-            if (!PE) { SG_PH(14); }
-            lds_barrier();
+            // reverse cumulative sums Q(k) = total - exclusive prefix (exact),
+            // the prefix and the total in registers (no LDS round trip, no
+            // barriers around one)
             {
-              const hyg_u128 tot = cum[NB], ex = cum[tid];
+              hyg_u128 ex, tot;
+              block_scan128_regs<NB>(mq, red, &ex, &tot);
+              if (!PE) { SG_PH(14); }
               hyg_u128 suf;
               suf.lo = tot.lo - ex.lo;
               suf.hi = tot.hi - ex.hi - (tot.lo < ex.lo ? 1u : 0u);
-              lds_barrier();
-              cum[tid] = suf;
               if (tid <= NT) logQ[tid] = hyg_log(hyg_u128_to_f64(suf, 100));
               if (NB == NT && tid == 0) logQ[NT] = HYG_NINF;
             }
@@ -920,13 +919,11 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
                 // sorted order (lqmono, checked for the K loop) it is position Kk's
                 const double rmax = lqmono ? logq[Kk] : block_max<NB>(inres ? lq : HYG_NINF, red);
                 const hyg_u128 m2 = inres ? hyg_exp_fix100(lq - rmax) : hyg_u128_zero();
-                block_scan128<NB>(m2, cum, red);
-                const hyg_u128 exv = cum[tid];  // C(p - 1) at sorted position p = tid
+                // C(p - 1) at sorted position p = tid, and R = C(Np - 1), the
+                // block total (m2 is 0 from Np on), in registers
+                hyg_u128 exv, R;
+                block_scan128_regs<NB>(m2, red, &exv, &R);
                 const hyg_u128 incl = hyg_u128_add(exv, m2);
-                lds_barrier();
-                cum[tid] = incl;
-                lds_barrier();
-                const hyg_u128 R = cum[Np - 1];
                 if (inres) {
                   // target j lands on the first position p >= Kk with C(p) >= ceil(T_j R):
                   // position p takes the targets j in [count(C(p - 1)), count(C(p)))
