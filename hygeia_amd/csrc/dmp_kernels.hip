@@ -292,12 +292,17 @@ int launch_post_counts(const float* split, const float* regime, int K2, int B, c
   if (n_seg <= 0 || max_rows <= 0) return 0;
   int64_t bx = (max_rows * (1 + K2) + 255) / 256;
   if (bx > 256) bx = 256;  // elements grid-strided: up to 256 x 256 threads per segment
-  if (exclusive)
-    hipLaunchKernelGGL(post_counts_kernel<true>, dim3((unsigned)bx, (unsigned)n_seg), dim3(256), 0,
-                       (hipStream_t)stream, split, regime, K2, (double)B, seg, counts);
-  else
-    hipLaunchKernelGGL(post_counts_kernel<false>, dim3((unsigned)bx, (unsigned)n_seg), dim3(256), 0,
-                       (hipStream_t)stream, split, regime, K2, (double)B, seg, counts);
+  constexpr int kMaxY = 65535;  // grid y limit: segments in launches of at most this many
+  for (int s0 = 0; s0 < n_seg; s0 += kMaxY) {
+    const int ns = (n_seg - s0 < kMaxY) ? n_seg - s0 : kMaxY;
+    const int64_t* sg = seg + 3 * (int64_t)s0;
+    if (exclusive)
+      hipLaunchKernelGGL(post_counts_kernel<true>, dim3((unsigned)bx, (unsigned)ns), dim3(256), 0,
+                         (hipStream_t)stream, split, regime, K2, (double)B, sg, counts);
+    else
+      hipLaunchKernelGGL(post_counts_kernel<false>, dim3((unsigned)bx, (unsigned)ns), dim3(256), 0,
+                         (hipStream_t)stream, split, regime, K2, (double)B, sg, counts);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
