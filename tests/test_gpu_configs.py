@@ -16,6 +16,10 @@ the CPU oracle, every output array compared):
 - C2 (configs[1]): one single-group chain of 200 000 sites at the pipeline
   settings (4 samples, K = 6, N_max = 250, epsilon = 0.01), long enough for the
   log-weights to reach the large-magnitude regime noted in DESIGN.md 1;
+- C2 at full length (round 6): the chromosome-1 chain of the C2 genome
+  (2 424 617 sites, the C2 bench's critical chain), with and without the
+  pipeline's online parameter estimation, against the oracle's digests
+  (tests/golden/sg_long_digest.json, made by tests/golden/make_sg_long.py);
 - C1 (configs[0]): the whole chr21-sized single-group chain (454 914 sites of
   the 28M-site genome), 2 samples, K = 6, N_max = 250,
   epsilon = 0.01, 1 seed, data from the single-group model (per-regime omega),
@@ -255,6 +259,82 @@ def test_c2_single_group_200k_chain(long_refs):
     bad = np.argwhere(out != ref["regime_probs"])
     assert bad.size == 0, (len(bad), bad[:5])
     np.testing.assert_allclose(out.sum(1), 1.0, atol=1e-8)
+
+
+def _sg_long_fixture():
+    import importlib.util
+    import json
+    import os
+
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    spec = importlib.util.spec_from_file_location("make_sg_long", os.path.join(here, "make_sg_long.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    with open(g.OUT) as f:
+        doc = json.load(f)
+    d = g.inputs()
+    assert g.input_digest(d) == doc["inputs"], "the input generator changed: regenerate the fixture"
+    return g, doc, d
+
+
+def _first_bad_blocks(got, ref):
+    return [i for i, (a, b) in enumerate(zip(got, ref)) if a != b][:5]
+
+
+@pytest.mark.timeout(900)
+def test_c2_chr1_chain():
+    """C2's critical chain at the length the pipeline runs it: chromosome 1 of
+    the 28 M genome (2 424 617 sites), 4 samples, K = 6, N_max = 250,
+    epsilon = 0.01, every regime probability bit-exact against the oracle's
+    digests (tests/golden/make_sg_long.py)."""
+    from hygeia_amd import _lib
+
+    g, doc, d = _sg_long_fixture()
+    ref = doc["chains"]["plain"]
+    p = _lib.SgParams.from_buffer_copy(bytes(g.params(False)))
+    out = _sg_host_chain(p, d["meth_control"], d["tot_control"], ref["seed"], ref["chain_id"])
+    got = g.output_record(out)
+    assert got["regime_probs"] == ref["regime_probs"], (
+        "chr1 chain differs from the oracle; first differing 100k-row blocks: "
+        f"{_first_bad_blocks(got['regime_probs_blocks'], ref['regime_probs_blocks'])}")
+
+
+@pytest.mark.timeout(1200)
+def test_c2_chr1_pe_chain():
+    """The pipeline's step 2 on the same chromosome-1 chain: online parameter
+    estimation (ADAM, an update every 200 steps, theta_0 from the prior), the
+    regime probabilities and all 12 124 theta rows bit-exact against the
+    oracle's digests."""
+    from hygeia_amd import _lib
+
+    g, doc, d = _sg_long_fixture()
+    ref = doc["chains"]["pe"]
+    L = _lib.load()
+    p = _lib.SgParams.from_buffer_copy(bytes(g.params(True)))
+    pe = _lib.SgPeParams()
+    L.hyg_sg_pe_params_default(C.byref(pe))
+    assert pe.n_steps_without_update == ref["every"]
+    meth = np.ascontiguousarray(d["meth_control"], np.uint16)
+    tot = np.ascontiguousarray(d["tot_control"], np.uint16)
+    T, S = tot.shape
+    h = C.c_void_p()
+    _lib.check(L.hyg_sg_model_create(C.byref(p), int(tot.max()), T + 10, C.byref(h)))
+    try:
+        out = np.full((T, 6), np.nan)
+        th = np.full((1 + (T - 1) // ref["every"], 36), np.nan)
+        rc = L.hyg_sg_run_chain_host_pe(h, C.byref(pe), meth.ctypes.data_as(C.c_void_p),
+                                        tot.ctypes.data_as(C.c_void_p), S, T, ref["seed"], ref["chain_id"],
+                                        out.ctypes.data_as(C.c_void_p), th.ctypes.data_as(C.c_void_p))
+        assert rc == 0, L.hyg_last_error()
+    finally:
+        L.hyg_sg_model_destroy(h)
+    got = g.output_record(out, th)
+    assert got["theta"] == ref["theta"], (
+        "theta rows differ from the oracle; first differing 1000-row blocks: "
+        f"{_first_bad_blocks(got['theta_blocks'], ref['theta_blocks'])}")
+    assert got["regime_probs"] == ref["regime_probs"], (
+        "regime probabilities differ from the oracle; first differing 100k-row blocks: "
+        f"{_first_bad_blocks(got['regime_probs_blocks'], ref['regime_probs_blocks'])}")
 
 
 @pytest.mark.timeout(600)
