@@ -316,8 +316,7 @@ def main():
         # all trajectories of all seeds (one HIP kernel over the chains' trimmed
         # rows), summed over ranks by one all-reduce
         # (one call per seed: a seed's chains cover disjoint sites, so no atomics)
-        tabs = [(torch.from_numpy(t).to(dev), int(t[:, 2].max())) for t in parallel.seed_tables(rebased, seg_of)]
-        runs.append((dcb, tabs))
+        runs.append((dcb, parallel.gather_tables(rebased, seg_of, dev)))
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
     E = torch.empty((args.sites, 2 * K), dtype=torch.float64, device=dev)
@@ -333,12 +332,8 @@ def main():
             _lib.check(L.hyg_tg_last_kernel_ms(ms3))
             kms += np.array(list(ms3)) * np.array([1.0 if i == 0 else 0.0, 1.0, 1.0])
         with torch.cuda.stream(stream):
-            counts.zero_()
-            for dcb, tabs in runs:
-                for tab, max_rows in tabs:
-                    parallel.posterior_counts_device(L, dcb.split_probs, dcb.regime_probs, B, tab, max_rows, counts,
-                                                     sp, exclusive=True)
-            parallel.allreduce_counts(counts)
+            parallel.gather_counts(L, [(dcb.split_probs, dcb.regime_probs, tabs) for dcb, tabs in runs], B, counts,
+                                   sp)
         return kms
 
     L.hyg_set_kernel_timing(1)

@@ -86,6 +86,43 @@ def seed_tables(chains, seg_of) -> List[np.ndarray]:
     return [segment_table([c for c in chains if c[2] == sd], seg_of) for sd in seeds]
 
 
+def disjoint_sites(table: np.ndarray) -> bool:
+    """True when the (output row, site, rows) entries of a segment table cover
+    pairwise disjoint site ranges, which the kernel's exclusive (atomic-free)
+    mode needs."""
+    if len(table) < 2:
+        return True
+    t = table[np.argsort(table[:, 1], kind="stable")]
+    return bool(np.all(t[:-1, 1] + t[:-1, 2] <= t[1:, 1]))
+
+
+def gather_tables(chains, seg_of, device) -> List[Tuple[object, int, bool]]:
+    """The job's gather plan for one launch's chains: per seed, the segment
+    table on `device` (int64 tensor), its longest row count and whether the
+    atomic-free mode applies (the seed's trimmed rows are disjoint; a table
+    whose rows overlap is summed with atomics instead of losing counts)."""
+    import torch
+
+    out = []
+    for t in seed_tables(chains, seg_of):
+        out.append((torch.from_numpy(t).to(device), int(t[:, 2].max()), disjoint_sites(t)))
+    return out
+
+
+def gather_counts(L, parts, B: int, counts, stream=0, always: bool = False):
+    """The job's final gather (aggregate_results.py:71-206) as bench.py runs it:
+    zero counts, add every launch's posterior counts with hyg_tg_posterior_counts
+    (one kernel per seed table), then sum over the ranks (allreduce_counts).
+    parts = [(split_probs, regime_probs, gather_tables(...)), ...] per launch;
+    the torch work runs on torch's current stream, which the caller sets to
+    `stream`. always: run the collective at world size 1 too (allreduce_counts)."""
+    counts.zero_()
+    for split, regime, tabs in parts:
+        for tab, max_rows, exclusive in tabs:
+            posterior_counts_device(L, split, regime, B, tab, max_rows, counts, stream, exclusive=exclusive)
+    return allreduce_counts(counts, always=always)
+
+
 def segment_table(chains, seg_of) -> np.ndarray:
     """int64 [n][3] (output row, site, rows) of the trimmed rows of each chain
     (site_begin, n_sites, seed, chain_id, out_begin); seg_of maps a chain id to
@@ -116,7 +153,38 @@ LOCK_DIR_VAR = "HYGEIA_DEVICE_LOCK_DIR"
 MAX_SLOTS_PER_DEVICE = 1024
 
 
-def task_device(L, n_devices: int = None, lock_dir: str = None, environ=None) -> Tuple[int, int]:
+def in_container(root: str = "/") -> bool:
+    """True inside a docker / podman container (the reference pipeline runs
+    every task in one, nextflow.config:31-34)."""
+    return any(os.path.exists(os.path.join(root, f)) for f in (".dockerenv", "run/.containerenv"))
+
+
+def default_lock_dir(environ=None, cwd: str = None) -> Tuple[str, str]:
+    """(directory, why) for the device slot locks when $HYGEIA_DEVICE_LOCK_DIR
+    is unset. A Nextflow task runs in <workDir>/<xx>/<hash> (its .command.sh
+    there); the pipeline's workDir is the one directory every task of the run
+    shares (Nextflow mounts it into each task container), so the slots go to
+    <workDir>/.hygeia_device_locks. Elsewhere: the temp directory, which is
+    private to a container."""
+    import tempfile
+
+    env = os.environ if environ is None else environ
+    cwd = cwd or os.getcwd()
+    task_dir = env.get("NXF_TASK_WORKDIR") or (cwd if os.path.exists(os.path.join(cwd, ".command.sh")) else None)
+    if task_dir:
+        work = os.path.dirname(os.path.dirname(os.path.abspath(task_dir)))
+        d = os.path.join(work, ".hygeia_device_locks")
+        try:
+            os.makedirs(d, exist_ok=True)
+            if os.access(d, os.W_OK):
+                return d, "nextflow"
+        except OSError:
+            pass
+    return tempfile.gettempdir(), "tmp"
+
+
+def task_device(L, n_devices: int = None, lock_dir: str = None, environ=None, container: bool = None,
+                cwd: str = None) -> Tuple[int, int]:
     """The device of one `hygeia infer` task process: (device, slot).
 
     The reference's Nextflow module starts one task process per (chrom, batch,
@@ -127,18 +195,24 @@ def task_device(L, n_devices: int = None, lock_dir: str = None, environ=None) ->
       ROCR_VISIBLE_DEVICES or CUDA_VISIBLE_DEVICES set) is obeyed: the task
       sees only those devices and takes the first (slot -1: no lock);
     - otherwise, with more than one device, the task takes a per-node slot
-      (hyg_device_slot_acquire: an exclusive flock in $HYGEIA_DEVICE_LOCK_DIR,
-      default the temp directory, which concurrent tasks must share -- mount one
-      host directory into every task container), the first free one in the
-      order slot 0 of every device, slot 1 of every device, ...: N concurrent
-      tasks spread N / n_devices per device, and a task that ends (or dies)
-      frees its slot for the next;
+      (hyg_device_slot_acquire: an exclusive flock in a directory every
+      concurrent task shares: $HYGEIA_DEVICE_LOCK_DIR, else the Nextflow run's
+      workDir inside a Nextflow task, else the temp directory), the first free
+      one in the order slot 0 of every device, slot 1 of every device, ...: N
+      concurrent tasks spread N / n_devices per device, and a task that ends
+      (or dies) frees its slot for the next;
+    - the temp directory of a container is private to it, so a task in a
+      container that falls back to it warns on stderr; and when no lock can be
+      taken at all the device is drawn at random (os.urandom), not from the
+      process id, which is the same small number in every container's PID
+      namespace;
     - with one device (or none), device 0.
 
-    n_devices / lock_dir / environ default to the live values; tests pass a fake
-    device count. Selecting the device (hyg_set_device) is the caller's."""
+    n_devices / lock_dir / environ / container / cwd default to the live
+    values; tests pass fake ones. Selecting the device (hyg_set_device) is the
+    caller's."""
     import ctypes as C
-    import tempfile
+    import sys
 
     env = os.environ if environ is None else environ
     if any(env.get(v, "").strip() for v in EXECUTOR_DEVICE_VARS):
@@ -146,9 +220,15 @@ def task_device(L, n_devices: int = None, lock_dir: str = None, environ=None) ->
     n = int(L.hyg_device_count()) if n_devices is None else int(n_devices)
     if n <= 1:
         return 0, -1
-    d = lock_dir or env.get(LOCK_DIR_VAR) or tempfile.gettempdir()
+    d = lock_dir or env.get(LOCK_DIR_VAR)
+    if not d:
+        d, why = default_lock_dir(env, cwd)
+        if why == "tmp" and (in_container() if container is None else container):
+            print(f"hygeia: warning: {n} GPUs but no shared lock directory: the device slots in {d} are private to "
+                  f"this container, so concurrent tasks may share one GPU; set {LOCK_DIR_VAR} to a host directory "
+                  "mounted into every task container", file=sys.stderr)
     dev, slot = C.c_int32(-1), C.c_int32(-1)
     rc = L.hyg_device_slot_acquire(d.encode(), n, MAX_SLOTS_PER_DEVICE, C.byref(dev), C.byref(slot))
-    if rc != 0:  # no shared lock directory: spread by process id instead of piling onto device 0
-        return os.getpid() % n, -1
+    if rc != 0:  # no usable lock directory: a random device, not the (namespaced) process id
+        return int.from_bytes(os.urandom(4), "little") % n, -1
     return int(dev.value), int(slot.value)

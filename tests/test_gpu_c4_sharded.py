@@ -3,10 +3,13 @@ modules/two_group/4_infer.nf:28) over two torch.distributed ranks on one GPU.
 
 The ranks are fresh processes (tests/c4_rank.py, "gloo": both share the one
 GPU of the test box) that each run their LPT shard of a fixed 3-seed job on a
-small genome through the chain kernels and all-reduce the per-site posterior
-counts. Required: the 2-rank counts equal the 1-rank run's (in this process)
-and the counts of the CPU oracle's chains, bit for bit. A second test runs the
-same collective through the "nccl" backend (RCCL) on the box's one GPU."""
+small genome through the code bench.py's SCALE runs execute: the chain kernels,
+the per-seed posterior-count kernel (hyg_tg_posterior_counts, atomic-free) and
+the all-reduce of the device counts (parallel.gather_counts). Required: the
+2-rank counts equal the 1-rank run's (in this process) and the counts of the CPU
+oracle's chains summed by torch (parallel.posterior_counts), bit for bit. A
+second test runs the same collective through the "nccl" backend (RCCL) on the
+box's one GPU."""
 import os
 import socket
 import subprocess
@@ -48,8 +51,10 @@ def _run_ranks(tmp_path, world, backend="gloo"):
 @pytest.mark.timeout(600)
 def test_c4_two_ranks_equal_one_rank_and_oracle(tmp_path):
     got = _run_ranks(tmp_path, 2)
-    one, units1, n_chains1, _ = c4_rank.rank_counts(0, 1)
+    one, units1, n_chains1, _, excl = c4_rank.rank_counts(0, 1)
     ref, units_ref = c4_rank.oracle_counts()
+    assert all(excl) and len(excl) == c4_rank.SEEDS  # one atomic-free gather per seed, as in bench.py
+    assert bool(np.all(got["exclusive"]))
     assert int(got["units"]) == units1 == units_ref == c4_rank.SEEDS * c4_rank.N_SITES
     assert int(got["chains"]) == n_chains1
     np.testing.assert_array_equal(got["counts"], one.numpy())
@@ -66,7 +71,7 @@ def test_c4_rccl_collective_one_rank(tmp_path):
     (the test box has one GPU; RCCL puts one rank per GPU), so the sum is the
     rank's own counts, which must equal the in-process run's bit for bit."""
     got = _run_ranks(tmp_path, 1, backend="nccl")
-    one, units1, n_chains1, _ = c4_rank.rank_counts(0, 1)
+    one, units1, n_chains1, _, _ = c4_rank.rank_counts(0, 1)
     assert str(got["backend"]) == "nccl"
     assert int(got["units"]) == units1 and int(got["chains"]) == n_chains1
     np.testing.assert_array_equal(got["counts"], one.numpy())

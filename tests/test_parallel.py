@@ -134,3 +134,21 @@ def test_segment_table_matches_row_lists():
     np.testing.assert_array_equal(np.concatenate([np.arange(s, s + n) for _, s, n in tab]), dst)
     # every site once per seed
     assert np.bincount(dst, minlength=900_000).tolist() == [2] * 900_000
+
+
+def test_gather_plan_is_exclusive_only_for_disjoint_seeds():
+    """parallel.disjoint_sites decides the gather kernel's atomic-free mode: a
+    seed's segments tile the genome without overlap (bench.py's plan), while a
+    table whose trimmed rows overlap is summed with atomics."""
+    from hygeia_amd import synthetic
+
+    segs = synthetic.segment_chains(synthetic.chromosome_sizes(900_000))
+    seg_of = {(ci << 32) | b: (s0, r0, rl) for (ci, b, s0, n, r0, rl) in segs}
+    chains = [(s0, n, sd, (ci << 32) | b, 0) for sd in (0, 1) for (ci, b, s0, n, r0, rl) in segs]
+    tabs = parallel.seed_tables(chains, seg_of)
+    assert len(tabs) == 2 and all(parallel.disjoint_sites(t) for t in tabs)
+    assert not parallel.disjoint_sites(parallel.segment_table(chains, seg_of))  # both seeds: every site twice
+    t = np.array([[0, 100, 50], [50, 10, 40], [90, 149, 3]], np.int64)  # unsorted, [149, 152) meets [100, 150)
+    assert not parallel.disjoint_sites(t)
+    t[2, 1] = 150
+    assert parallel.disjoint_sites(t) and parallel.disjoint_sites(t[:1]) and parallel.disjoint_sites(t[:0])
