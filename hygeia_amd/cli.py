@@ -395,7 +395,12 @@ def _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c,
     torch: the library is loaded without it (a fresh task saves its import)."""
     from . import _lib, two_group
 
-    _use_task_device(_lib.load(import_torch=False))  # (raises without the HIP library)
+    L = _lib.load(import_torch=False)  # (raises without the HIP library)
+    _use_task_device(L)
+    # tools/bench_pipeline.py: the kernels' own time (HIP events) beside the wall
+    timing = os.environ.get("HYGEIA_TASK_TIMING") == "1"
+    if timing:
+        L.hyg_set_kernel_timing(1)
 
     for M in f["num_resampled_particles"]:
         print(M)
@@ -413,6 +418,12 @@ def _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c,
             model.close()
         times[N] = time.time() - t0
         LAST_TIMINGS["chains"] = LAST_TIMINGS.get("chains", 0.0) + times[N]  # (inside "device")
+        if timing:
+            import ctypes as C
+
+            ms3 = (C.c_float * 3)()
+            if L.hyg_tg_last_kernel_ms(ms3) == 0:
+                LAST_TIMINGS["kernels"] = LAST_TIMINGS.get("kernels", 0.0) + sum(x for x in ms3 if x > 0) / 1000.0
         log_z[N] = float(ex["log_z"])
         pr = res.particle
         for name, arr in ((f"optimal_backward_particles_merged_state_{N}_{seed}",
@@ -631,9 +642,10 @@ def main(argv: Sequence[str] = None) -> int:
             print(f"Error: {e}", file=sys.stderr)
             return 1
     if cmd in ("version", "-v", "--version"):
-        from . import _lib
-        print("Hygeia version {} ({})".format(os.environ.get("HYGEIA_VERSION", ""),
-                                              _lib.load().hyg_version().decode()))
+        # every 4_infer.nf task runs this for versions.yml (:54-57): no torch
+        # import, no HIP library load (_lib.VERSION equals hyg_version())
+        from ._lib import VERSION
+        print("Hygeia version {} ({})".format(os.environ.get("HYGEIA_VERSION", ""), VERSION))
         return 0
     if cmd in ("help", "-h", "--help"):
         print("Usage: hygeia [command] [arguments...]\n  preprocess - Preprocess BED methylation files (MI355X)\n"

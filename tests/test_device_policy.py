@@ -74,7 +74,7 @@ def test_single_device_and_unusable_lock_dir(tmp_path):
     L = _lib.load(import_torch=False)
     assert parallel.task_device(L, n_devices=1, lock_dir=str(tmp_path), environ={}) == (0, -1)
     dev, slot = parallel.task_device(L, n_devices=8, lock_dir=str(tmp_path / "missing"), environ={})
-    assert slot == -1 and 0 <= dev < 8  # spread by process id
+    assert slot == -1 and 0 <= dev < 8  # a random device
     import ctypes as C
 
     d, s = C.c_int32(), C.c_int32()
@@ -86,3 +86,34 @@ def test_set_device_without_gpu_fails_loudly():
     if L.hyg_device_count() > 0:
         pytest.skip("a GPU is visible")
     assert L.hyg_set_device(0) == _lib.HYG_EDEVICE
+
+
+def test_nextflow_task_defaults_to_the_shared_work_dir(tmp_path, capsys):
+    """Inside a Nextflow task (.command.sh in the working directory
+    <workDir>/<xx>/<hash>), the slots go to <workDir>/.hygeia_device_locks,
+    which every task of the run shares (and no warning is printed)."""
+    L = _lib.load(import_torch=False)
+    tasks = [tmp_path / "work" / "ab" / h for h in ("cdef01", "cdef02")]
+    for t in tasks:
+        t.mkdir(parents=True)
+        (t / ".command.sh").write_text("hygeia infer\n")
+    try:
+        assert parallel.task_device(L, n_devices=4, environ={}, container=True, cwd=str(tasks[0])) == (0, 0)
+        assert os.listdir(tmp_path / "work" / ".hygeia_device_locks") == ["hygeia_amd.gpu0.slot0.lock"]
+    finally:
+        assert L.hyg_device_slot_release() == 0
+    assert "warning" not in capsys.readouterr().err
+    d, why = parallel.default_lock_dir({"NXF_TASK_WORKDIR": str(tasks[1])}, cwd=str(tmp_path))
+    assert why == "nextflow" and d == str(tmp_path / "work" / ".hygeia_device_locks")
+    assert parallel.default_lock_dir({}, cwd=str(tmp_path))[1] == "tmp"
+
+
+def test_container_without_shared_lock_dir_warns(tmp_path, capsys):
+    L = _lib.load(import_torch=False)
+    try:
+        parallel.task_device(L, n_devices=4, environ={}, container=True, cwd=str(tmp_path))
+        assert "no shared lock directory" in capsys.readouterr().err
+        parallel.task_device(L, n_devices=4, environ={}, container=False, cwd=str(tmp_path))
+        assert capsys.readouterr().err == ""
+    finally:
+        assert L.hyg_device_slot_release() == 0

@@ -74,19 +74,29 @@ DRIVER = ("import json, sys, time; t0 = time.perf_counter(); from hygeia_amd imp
           "device=cli.LAST_DEVICE.get('device', -1), slot=cli.LAST_DEVICE.get('slot', -1))), flush=True)")
 
 
-def run_task(args, env=None) -> dict:
+def run_task(args, env=None, version=False) -> dict:
+    """One task as a fresh process; version: then `hygeia --version` as
+    4_infer.nf:54-57 runs it after every task, inside the task's wall."""
     t0 = time.perf_counter()
-    r = subprocess.run([sys.executable, "-c", DRIVER] + list(args), cwd=ROOT, capture_output=True, text=True,
-                       env=dict(os.environ if env is None else env, PYTHONPATH=ROOT))
+    e = dict(os.environ if env is None else env, PYTHONPATH=ROOT, HYGEIA_TASK_TIMING="1")
+    r = subprocess.run([sys.executable, "-c", DRIVER] + list(args), cwd=ROOT, capture_output=True, text=True, env=e)
     t1 = time.perf_counter()
     if r.returncode != 0:
         raise RuntimeError(f"hygeia {' '.join(args[:5])} failed: {r.stderr[-2000:]}")
     split = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("@@")][-1][2:])
-    return {"start": t0, "end": t1, "wall_s": t1 - t0, "split": split}
+    if version:
+        v = subprocess.run([os.path.join(ROOT, "bin", "hygeia"), "--version"], cwd=ROOT, capture_output=True,
+                           text=True, env=e)
+        if v.returncode != 0 or "Hygeia version" not in v.stdout:
+            raise RuntimeError(f"hygeia --version failed: {v.stderr[-500:]}")
+        split["version"] = time.perf_counter() - t1
+    t2 = time.perf_counter()
+    return {"start": t0, "end": t2, "wall_s": t2 - t0, "split": split}
 
 
-def concurrent_sweep(wd, common, seeds, sites, n_batches, ns):
-    """Every (batch, seed) task as a fresh `hygeia infer` process, N at a time."""
+def concurrent_sweep(wd, common, seeds, sites, n_batches, ns, env=None):
+    """Every (batch, seed) task as a fresh `hygeia infer` process followed by
+    `hygeia --version` (the module's script), N at a time."""
     from concurrent.futures import ThreadPoolExecutor
 
     units = sites * len(seeds)
@@ -97,7 +107,8 @@ def concurrent_sweep(wd, common, seeds, sites, n_batches, ns):
 
         def one(t):
             b, sd = t
-            r = run_task(["infer", "--batch", str(b), "--seed", str(sd), "--results_dir", rdir] + common)
+            r = run_task(["infer", "--batch", str(b), "--seed", str(sd), "--results_dir", rdir] + common, env=env,
+                         version=True)
             print(f"  N={n} batch {b} seed {sd}: {r['wall_s']:.2f} s", file=sys.stderr, flush=True)  # progress
             return r
 
@@ -107,9 +118,13 @@ def concurrent_sweep(wd, common, seeds, sites, n_batches, ns):
         wall = time.perf_counter() - t0
         walls = np.array([r["wall_s"] for r in res])
         chains = np.array([r["split"].get("chains", 0.0) for r in res])
+        kern = np.array([r["split"].get("kernels", 0.0) for r in res])
+        ver = np.array([r["split"].get("version", 0.0) for r in res])
         rec = {"concurrent": n, "tasks": len(tasks), "wall_s": wall, "value": units / wall,
                "task_wall_s": {"mean": float(walls.mean()), "min": float(walls.min()), "max": float(walls.max())},
                "task_chains_s": {"mean": float(chains.mean()), "max": float(chains.max())},
+               "task_kernels_s": {"mean": float(kern.mean()), "max": float(kern.max())},
+               "task_version_s": {"mean": float(ver.mean()), "max": float(ver.max())},
                "devices": sorted({(r["split"]["device"], r["split"]["slot"]) for r in res})}
         out.append(rec)
         print(json.dumps(rec), flush=True)
@@ -123,6 +138,8 @@ def main():
     ap.add_argument("--seeds", default="0,1")
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--concurrent", default="", help="comma list of N: every task as a process, N at once")
+    ap.add_argument("--task-env", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra environment of the task processes (e.g. GPU_MAX_HW_QUEUES=1)")
     a = ap.parse_args()
     if a.concurrent:
         return main_concurrent(a)
@@ -191,11 +208,13 @@ def main_concurrent(a):
     many = run_task(["infer_many", "--batches", "all", "--seeds", a.seeds, "--results_dir",
                      os.path.join(wd, "many")] + common)
     print(f"infer_many {many['wall_s']:.1f} s", flush=True)
-    sweep = concurrent_sweep(wd, common, seeds, a.sites, n_batches, [int(x) for x in a.concurrent.split(",")])
+    env = dict(os.environ)
+    env.update(kv.split("=", 1) for kv in a.task_env)
+    sweep = concurrent_sweep(wd, common, seeds, a.sites, n_batches, [int(x) for x in a.concurrent.split(",")], env)
     line = {"metric": "pipeline CpG sites x seeds / s (hygeia infer, gz CSV in -> result files out)",
             "sites": a.sites, "seeds": seeds, "tasks": n_batches * len(seeds),
             "infer_many": {"value": units / many["wall_s"], "wall_s": many["wall_s"], "split_s": many["split"]},
-            "concurrent_tasks": sweep,
+            "concurrent_tasks": sweep, "task_env": a.task_env,
             "note": "each task a fresh `hygeia infer` process, N at once on one GPU (Nextflow local executor)"}
     print(json.dumps(line), flush=True)
     if a.workdir is None:
