@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libtg_oracle.so")
+# HYG_ORACLE_DIR=build_san: the sanitizer build (make SAN=1, tools/sanitize.sh)
+LIB_PATH = os.path.join(HERE, os.environ.get("HYG_ORACLE_DIR", "build"), "libtg_oracle.so")
 KMAX = 16
 
 # pipeline defaults (run_inference_two_groups.py:19-36, nextflow.config)

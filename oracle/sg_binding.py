@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libsg_oracle.so")
+# HYG_ORACLE_DIR=build_san: the sanitizer build (make SAN=1, tools/sanitize.sh)
+LIB_PATH = os.path.join(HERE, os.environ.get("HYG_ORACLE_DIR", "build"), "libsg_oracle.so")
 KMAX = 16
 
 # pipeline defaults: regimes_config / nextflow.config, bin/simulate_data:147-157
