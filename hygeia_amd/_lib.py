@@ -113,7 +113,8 @@ class SgChain(C.Structure):
 
 
 EXPORTS = ("hyg_tg_params_default", "hyg_tg_model_create", "hyg_tg_model_destroy", "hyg_tg_num_particles",
-           "hyg_tg_threads_per_chain", "hyg_tg_force_threads", "hyg_tg_set_tail_overlap", "hyg_sg_force_key_drop", "hyg_tg_chains_per_cu", "hyg_tg_lds_bytes",
+           "hyg_tg_threads_per_chain", "hyg_tg_force_threads", "hyg_tg_set_tail_overlap", "hyg_tg_device_cus",
+           "hyg_tg_set_device_cus", "hyg_sg_force_key_drop", "hyg_tg_chains_per_cu", "hyg_tg_lds_bytes",
            "hyg_tg_emission", "hyg_tg_workspace_bytes", "hyg_tg_run_chains", "hyg_tg_run_chain_host",
            "hyg_tg_run_chains_host",
            "hyg_device_count", "hyg_device_slot_acquire", "hyg_device_slot_release", "hyg_set_device",
@@ -132,6 +133,10 @@ class DmpGroup(C.Structure):
 
 _lib = None
 
+# The library's version string (hyg_version(), capi.cpp); `hygeia --version`
+# prints it without loading the library (tests/test_capi_cpu.py pins the two
+# equal).
+VERSION = "hygeia_amd 0.1.0 (gfx950)"
 
 _with_torch = False  # whether torch was imported before the library loaded
 
@@ -184,6 +189,10 @@ def load(import_torch: bool = True) -> C.CDLL:
     L.hyg_tg_force_threads.argtypes = [i32, i32]
     L.hyg_tg_set_tail_overlap.restype = C.c_int
     L.hyg_tg_set_tail_overlap.argtypes = [i32]
+    L.hyg_tg_device_cus.restype = i32
+    L.hyg_tg_device_cus.argtypes = [i32]
+    L.hyg_tg_set_device_cus.restype = C.c_int
+    L.hyg_tg_set_device_cus.argtypes = [i32, i32]
     L.hyg_sg_force_key_drop.restype = C.c_int
     L.hyg_sg_force_key_drop.argtypes = [i32]
     L.hyg_tg_chains_per_cu.restype = i32

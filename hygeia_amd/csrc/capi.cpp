@@ -385,6 +385,13 @@ int hyg_tg_set_tail_overlap(int32_t on) {
   return HYG_OK;
 }
 
+int32_t hyg_tg_device_cus(int32_t device) { return hyg::tg_device_cus(device); }
+
+int hyg_tg_set_device_cus(int32_t device, int32_t cus) {
+  const int rc = hyg::tg_set_device_cus(device, cus);
+  return rc == HYG_OK ? rc : fail(rc, "device out of [0, 64) or negative CU count");
+}
+
 int hyg_sg_force_key_drop(int32_t bits) {
   const int rc = hyg::sg_force_key_drop(bits);
   return rc == HYG_OK ? rc : fail(rc, "key bits out of range [8, 60]");

@@ -1062,6 +1062,9 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       // particle n and thread 256 + n rows [KH, K) (it recomputes e_n); threads
       // 256 .. 256 + K^2 form G.
       constexpr bool SPLIT = (NB == 2 * NT);
+      // the G wave below is one wave (64 lanes) forming the K^2 entries of G:
+      // the 512-thread build is dispatched for K <= 8 only (SG_CASE)
+      static_assert(!SPLIT || K * K <= 64, "the split build's single G wave holds at most 64 entries");
       constexpr int KH = SPLIT ? (K + 1) / 2 : K;
       const int pn = SPLIT ? (tid & (NT - 1)) : tid;  // the previous particle of this thread
       const int q0 = (SPLIT && tid >= NT) ? KH : 0;   // wave-uniform

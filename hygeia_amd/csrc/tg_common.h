@@ -81,6 +81,8 @@ int tg_threads_per_chain(const hyg_tg_consts& c, int n_chains);  // forward work
 int tg_force_threads(int fwd, int bwd);                           // test override (0 = automatic)
 int tg_resident_per_cu(const hyg_tg_consts& c, int n_chains);     // forward workgroups per CU
 void tg_set_tail_overlap(bool on);                                // hyg_tg_set_tail_overlap
+int tg_device_cus(int dev);                                       // CUs of a device as the launcher sees them
+int tg_set_device_cus(int dev, int cus);                          // test override (0 = query the device)
 size_t tg_layout_bytes(const hyg_tg_consts& c, int threads, bool backward);  // LDS of one chain (0: bad width)
 // Whether a model's backward keeps its full-N weights (the general path and the
 // final step's draw) in a per-chain global scratch of Nmax f64 instead of LDS,

@@ -22,6 +22,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -2692,28 +2693,58 @@ tg_backward_kernel(ModelDev md, const ChainDev* __restrict__ chains, const doubl
 
 // -------------------------------------------------------------- launchers
 // Optional per-kernel timing with HIP events recorded on the launch stream
-// (bench.py reads them back with hyg_tg_last_kernel_ms).
+// (bench.py reads them back with hyg_tg_last_kernel_ms). The events belong to
+// the device they were created on and are recreated when the calling thread's
+// device changes; one mutex orders every use of them.
 namespace {
+std::mutex g_ev_mu;
 bool g_timing = false;
+int g_ev_dev = -1;
 hipEvent_t g_ev[6] = {};
 bool g_ev_used[3] = {false, false, false};
 void ev_record(int k, bool end, hipStream_t s) {
+  std::lock_guard<std::mutex> lock(g_ev_mu);
   if (!g_timing) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  if (dev != g_ev_dev) {  // new device: the old device's events cannot be recorded here
+    for (int i = 0; i < 6; ++i) {
+      if (g_ev[i]) (void)hipEventDestroy(g_ev[i]);
+      g_ev[i] = nullptr;
+    }
+    for (int i = 0; i < 3; ++i) g_ev_used[i] = false;
+    g_ev_dev = dev;
+  }
   hipEvent_t& e = g_ev[2 * k + (end ? 1 : 0)];
   if (!e) (void)hipEventCreate(&e);
   (void)hipEventRecord(e, s);
   g_ev_used[k] = true;
 }
+// CUs of each device (the launch-width and tail-overlap choices depend on
+// them), cached per device: a process that switches devices (hyg_set_device)
+// sees each device's own count. hyg_tg_set_device_cus overrides an entry
+// (tests fake devices of other sizes); 0 = unknown / query again.
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_cus[kMaxDevices];
+int query_cus(int dev) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 0;
+  return n;
+}
+int cus_of(int dev) {
+  if (dev < 0) return 0;
+  if (dev >= kMaxDevices) return query_cus(dev);
+  int n = g_cus[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  n = query_cus(dev);
+  if (n > 0) g_cus[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
 int device_cus() {
-  static int cus = -1;
-  if (cus < 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || n <= 0)
-      n = 256;
-    cus = n;
-  }
-  return cus;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  const int n = cus_of(dev);
+  return n > 0 ? n : 256;
 }
 // Threads per chain workgroup. HYG_THREADS (or HYG_THREADS_FWD / _BWD) if set.
 // Otherwise by what the launch's chains leave of the GPU:
@@ -2769,9 +2800,20 @@ int tg_force_threads(int fwd, int bwd) {
   return HYG_OK;
 }
 
-void set_kernel_timing(bool on) { g_timing = on; }
+int tg_device_cus(int dev) { return cus_of(dev); }
+int tg_set_device_cus(int dev, int cus) {
+  if (dev < 0 || dev >= kMaxDevices || cus < 0) return HYG_EINVAL;
+  g_cus[dev].store(cus, std::memory_order_relaxed);
+  return HYG_OK;
+}
+
+void set_kernel_timing(bool on) {
+  std::lock_guard<std::mutex> lock(g_ev_mu);
+  g_timing = on;
+}
 
 int last_kernel_ms(float* out3) {
+  std::lock_guard<std::mutex> lock(g_ev_mu);
   for (int k = 0; k < 3; ++k) {
     out3[k] = -1.0f;
     if (!g_ev_used[k] || !g_ev[2 * k] || !g_ev[2 * k + 1]) continue;
@@ -3095,15 +3137,28 @@ int launch_chains(const ModelDev& md, const hyg_tg_consts& c, const ChainDev* ch
   rc = launch_forward(ntf, md, c, chains_dev + head, tail, E, ws, out_t, s, false);
   if (rc != HYG_OK) return rc;
   ev_record(1, true, s);
-  if (hipStreamWaitEvent(aux->s, aux->head_done, 0) != hipSuccess) return HYG_EDEVICE;
+  // From here the second stream holds work: every return path below makes the
+  // launch stream wait for it, so the call's stream covers the whole launch
+  // whatever fails.
+  auto join = [&](int code) {
+    const bool ok = hipEventRecord(aux->bwd_done, aux->s) == hipSuccess &&
+                    hipStreamWaitEvent(s, aux->bwd_done, 0) == hipSuccess;
+    if (code == HYG_OK && !ok) return (int)HYG_EDEVICE;
+    if (!ok) (void)hipStreamSynchronize(aux->s);  // the events failed: drain the second stream instead
+    return code;
+  };
+  if (hipStreamWaitEvent(aux->s, aux->head_done, 0) != hipSuccess) return join(HYG_EDEVICE);
+  // The guard kernel is a scheduling heuristic, not a dependency: it only makes
+  // the tail's forward (released by head_done on the launch stream) likely to
+  // take its CUs before the head's backward fills them. The outputs do not
+  // depend on which dispatch wins.
   hipLaunchKernelGGL(tg_dispatch_guard_kernel, dim3(1), dim3(64), 0, aux->s);
   ev_record(2, false, aux->s);
   rc = launch_backward(ntb, md, c, chains_dev, head, E, ws, out, aux->s, false);
-  if (rc != HYG_OK) return rc;
-  if (hipEventRecord(aux->bwd_done, aux->s) != hipSuccess) return HYG_EDEVICE;
+  if (rc != HYG_OK) return join(rc);
   rc = launch_backward(ntb, md, c, chains_dev + head, tail, E, ws, out_t, s, false);
+  rc = join(rc);
   if (rc != HYG_OK) return rc;
-  if (hipStreamWaitEvent(s, aux->bwd_done, 0) != hipSuccess) return HYG_EDEVICE;
   ev_record(2, true, s);
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }

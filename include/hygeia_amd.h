@@ -145,6 +145,19 @@ int hyg_tg_force_threads(int32_t forward, int32_t backward);
  * do not depend on it (GPU test). Not thread-safe. No reference counterpart. */
 int hyg_tg_set_tail_overlap(int32_t on);
 
+/* Compute units of `device` as the two-group launcher sees them: the width
+ * choice (one chain per CU or more) and the tail overlap depend on it. Cached
+ * per device, so a process that switches devices (hyg_set_device) uses each
+ * device's own count. 0 if unknown (no such device, no HIP). No reference
+ * counterpart. */
+int32_t hyg_tg_device_cus(int32_t device);
+
+/* Test override of that count for device (0 <= device < 64); cus = 0 drops
+ * the override (the next use queries the device). The results do not depend
+ * on it (every width computes the same bits); launches after it are shaped as
+ * on a device with that many CUs. */
+int hyg_tg_set_device_cus(int32_t device, int32_t cus);
+
 /* Test override of the single-group chain's log-weight sort for every later
  * launch in the process. The sort orders one 64-bit word per particle: the
  * order key's top 64 - bits bits and the particle index (bits = 8, or 0 for
@@ -162,7 +175,12 @@ int hyg_tg_emission(const hyg_tg_model* model, const uint16_t* meth_ctrl, const 
                     int64_t n_sites, double* emission, void* stream);
 
 /* Workspace bytes for the forward->backward ancestor history of `n_chains`
- * chains totalling `total_steps` filter steps. */
+ * chains totalling `total_steps` filter steps. For the K = 12 stress shape the
+ * bound also holds a full-N weight scratch per chain (Nmax f64, 67 KB), which
+ * only the 256-thread backward of a launch with more chains than CUs uses; it
+ * is charged whatever the width, so the size does not depend on the launch
+ * width or hyg_tg_force_threads (a conservative bound: under 0.04 % of a
+ * full-length chain's history). */
 size_t hyg_tg_workspace_bytes(const hyg_tg_model* model, int32_t n_chains, int64_t total_steps);
 
 /* Outputs of hyg_tg_run_chains, all device pointers indexed by out_begin + t:

@@ -33,6 +33,27 @@ def test_exports_every_declared_symbol(lib):
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.EXPORTS)
     assert lib.hyg_version().decode().startswith("hygeia_amd")
+    assert lib.hyg_version().decode() == _lib.VERSION  # what `hygeia --version` prints without loading it
+
+
+def test_device_cus_cached_per_device(lib):
+    """The launcher's CU count is kept per device (hyg_set_device may switch
+    between GPUs of different sizes): two faked devices keep their own counts,
+    and dropping an override leaves the other in place."""
+    try:
+        assert lib.hyg_tg_set_device_cus(0, 256) == 0 and lib.hyg_tg_set_device_cus(1, 64) == 0
+        assert lib.hyg_tg_device_cus(0) == 256 and lib.hyg_tg_device_cus(1) == 64
+        assert lib.hyg_tg_set_device_cus(1, 80) == 0
+        assert lib.hyg_tg_device_cus(0) == 256 and lib.hyg_tg_device_cus(1) == 80
+        assert lib.hyg_tg_set_device_cus(0, 0) == 0
+        assert lib.hyg_tg_device_cus(1) == 80
+        if lib.hyg_device_count() == 0:
+            assert lib.hyg_tg_device_cus(0) == 0  # no HIP device: unknown
+        assert lib.hyg_tg_set_device_cus(-1, 4) == -1 and lib.hyg_tg_set_device_cus(64, 4) == -1
+        assert lib.hyg_tg_set_device_cus(0, -4) == -1
+    finally:
+        lib.hyg_tg_set_device_cus(0, 0)
+        lib.hyg_tg_set_device_cus(1, 0)
 
 
 def test_params_default_matches_reference_flags(lib):

@@ -148,6 +148,16 @@ def test_width_selection_by_chains_per_cu():
     m12 = two_group.CaseControlModel(mu, sg, two_group.uniform_theta(12), max_total_reads=200, max_duration=100)
     assert L.hyg_tg_threads_per_chain(m12.handle, 10) == 512
     assert L.hyg_tg_threads_per_chain(m12.handle, 1164) == 512
+    # the choice follows the current device's own CU count (cached per device):
+    # on a faked 64-CU device 100 chains are more than one per CU
+    assert L.hyg_tg_device_cus(0) == cus
+    try:
+        assert L.hyg_tg_set_device_cus(0, 64) == 0
+        assert [L.hyg_tg_threads_per_chain(m6.handle, n) for n in (64, 100)] == [512, 256]
+    finally:
+        L.hyg_tg_set_device_cus(0, 0)
+    assert L.hyg_tg_device_cus(0) == cus
+    assert [L.hyg_tg_threads_per_chain(m6.handle, n) for n in (64, 100)] == [512, 512]
 
 
 def test_zero_coverage_stretch(oracle):
@@ -432,3 +442,4 @@ def test_tail_overlap_equals_one_launch(oracle):
             np.testing.assert_array_equal(a[k][o0:o0 + n], ref[k], err_msg=f"chain {i} {k}")
         assert a["log_z"][i] == ref["log_z"]
         np.testing.assert_array_equal(a["final_w"][i], ref["final_log_weights"])
+
