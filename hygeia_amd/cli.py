@@ -26,6 +26,7 @@ from __future__ import annotations
 import gzip
 import math
 import os
+import re
 import sys
 import time
 import zlib
@@ -155,9 +156,40 @@ def chain_id(chrom: str, batch: int) -> int:
     return (zlib.crc32(str(chrom).encode()) << 32) | (int(batch) & 0xFFFFFFFF)
 
 
-def _read_matrix(path: str) -> np.ndarray:
+def _gz_prefix(path: str, max_rows: int):
+    """(the bytes of the first max_rows lines of a (multi-member) gzip file,
+    whether the file goes on past them). Decompression is most of a parse."""
+    import zlib
+
+    out, lines, more = [], 0, False
+    with open(path, "rb") as fh:
+        d = zlib.decompressobj(wbits=47)  # gzip or zlib header, auto-detected
+        while True:
+            c = fh.read(1 << 20)
+            if not c:
+                break
+            while c:
+                x = d.decompress(c)
+                if x:
+                    k = x.count(b"\n")
+                    if lines + k >= max_rows:
+                        nl = np.flatnonzero(np.frombuffer(x, np.uint8) == 10)
+                        cut = int(nl[max_rows - lines - 1]) + 1
+                        out.append(x[:cut])
+                        return b"".join(out), True
+                    lines += k
+                    out.append(x)
+                c = d.unused_data  # the next gzip member
+                if c:
+                    d = zlib.decompressobj(wbits=47)
+        out.append(d.flush())
+    return b"".join(out), more
+
+
+def _read_matrix(path: str, max_rows: int = None) -> np.ndarray:
     """A whole-chromosome count matrix (run_inference_two_groups.py:177-191 reads
-    it with pd.read_table(sep=",", header=None)) as float64.
+    it with pd.read_table(sep=",", header=None)) as float64; with max_rows, only
+    its first max_rows rows (the file is decompressed no further).
 
     Parsed by pyarrow's multi-threaded CSV reader (about 2.7x pandas on a chr1
     matrix, most of a single `hygeia infer` task's host time). The pipeline's
@@ -166,11 +198,22 @@ def _read_matrix(path: str) -> np.ndarray:
     non-integral or non-finite value (or one pyarrow cannot read) is re-read
     with pandas, the reference's parser, so such input keeps its exact values.
     (pandas is imported on that path only.)"""
+    import io
+
     try:
         import pyarrow.csv as pacsv
 
-        tb = pacsv.read_csv(path, read_options=pacsv.ReadOptions(autogenerate_column_names=True),
-                            parse_options=pacsv.ParseOptions(delimiter=","))
+        ro = pacsv.ReadOptions(autogenerate_column_names=True)
+        po = pacsv.ParseOptions(delimiter=",")
+        if max_rows is None or not path.endswith(".gz"):
+            tb = pacsv.read_csv(path, read_options=ro, parse_options=po)
+        else:
+            raw, more = _gz_prefix(path, max_rows)
+            tb = pacsv.read_csv(io.BytesIO(raw), read_options=ro, parse_options=po)
+            if more and tb.num_rows < max_rows:  # blank lines were among the lines cut: read it all
+                tb = pacsv.read_csv(path, read_options=ro, parse_options=po)
+        if max_rows is not None:
+            tb = tb.slice(0, max_rows)
         cols = [c.to_numpy(zero_copy_only=False) for c in tb.columns]
         if tb.num_columns > 0 and all(c.dtype.kind in "iuf" for c in cols):
             a = np.column_stack(cols).astype(np.float64)
@@ -180,29 +223,168 @@ def _read_matrix(path: str) -> np.ndarray:
         pass  # ArrowTypeError, ...) falls back to pandas, the reference's parser
     import pandas as pd
 
-    return pd.read_csv(path, sep=",", header=None, dtype=np.float64).to_numpy()
+    return pd.read_csv(path, sep=",", header=None, dtype=np.float64, nrows=max_rows).to_numpy()
 
 
-def _read_inputs(data_dir: str, chrom: str):
+PARSE_CACHE_VAR = "HYGEIA_PARSE_CACHE"
+
+
+def parse_cache_dir(environ=None, cwd: str = None):
+    """Where parsed input matrices are kept for the next task of the same
+    chromosome: $HYGEIA_PARSE_CACHE ("0": none), else inside a Nextflow task
+    (.command.sh in the working directory <workDir>/<xx>/<hash>) the run's
+    <workDir>/.hygeia_parse_cache, else none. Every (batch, seed) task of a
+    chromosome reads the same five gzip files (4_infer.nf:28); with the cache
+    one of them decompresses and parses each file and the others map the
+    result."""
+    env = os.environ if environ is None else environ
+    v = env.get(PARSE_CACHE_VAR, "").strip()
+    if v == "0":
+        return None
+    if v:
+        return v
+    cwd = cwd or os.getcwd()
+    task = env.get("NXF_TASK_WORKDIR") or (cwd if os.path.exists(os.path.join(cwd, ".command.sh")) else None)
+    if task:
+        return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(task))), ".hygeia_parse_cache")
+    return None
+
+
+def _cached_matrix(path: str, cache: str, max_rows: int = None) -> np.ndarray:
+    """_read_matrix through the parse cache: the whole file's matrix is parsed
+    once (under an exclusive lock, so concurrent tasks wait for it rather than
+    parse it too) and kept as an .npy keyed by the file's path, size, mtime and
+    inode (int32 when every value fits, else float64: the values are those of
+    the parse); a task maps it and copies its rows out. Any cache failure reads
+    the file directly."""
+    import fcntl
+    import hashlib
+
+    try:
+        st = os.stat(path)
+        key = hashlib.sha1(f"{os.path.realpath(path)}|{st.st_size}|{st.st_mtime_ns}|{st.st_ino}".encode()).hexdigest()
+        os.makedirs(cache, exist_ok=True)
+        npy = os.path.join(cache, key + ".npy")
+        if not os.path.exists(npy):
+            with open(os.path.join(cache, key + ".lock"), "a") as lk:
+                fcntl.flock(lk, fcntl.LOCK_EX)
+                if not os.path.exists(npy):
+                    a = _read_matrix(path)
+                    small = a.size == 0 or (a.min() >= -2 ** 31 and a.max() < 2 ** 31)
+                    tmp = npy + f".{os.getpid()}.tmp.npy"
+                    np.save(tmp, a.astype(np.int32) if small else a)
+                    os.replace(tmp, npy)
+                    return a if max_rows is None else a[:max_rows]
+        m = np.load(npy, mmap_mode="r")
+        return np.asarray(m if max_rows is None else m[:max_rows], dtype=np.float64)
+    except OSError:
+        return _read_matrix(path, max_rows)
+
+
+def _read_inputs(data_dir: str, chrom: str, max_rows: int = None):
     """positions, n_total_reads_control, n_methylated_reads_control,
     n_total_reads_case, n_methylated_reads_case of one chromosome
     (run_inference_two_groups.py:177-191), the five files read concurrently
-    (each file's gzip stream decompresses on one thread)."""
+    (each file's gzip stream decompresses on one thread); with max_rows, the
+    first max_rows rows of each; through the parse cache when there is one
+    (parse_cache_dir)."""
     from concurrent.futures import ThreadPoolExecutor
 
     names = ["positions", "n_total_reads_control", "n_methylated_reads_control", "n_total_reads_case",
              "n_methylated_reads_case"]
     paths = [os.path.join(data_dir, f"{n}_{chrom}.txt.gz") for n in names]
+    cache = parse_cache_dir()
+    read = (lambda p: _cached_matrix(p, cache, max_rows)) if cache else (lambda p: _read_matrix(p, max_rows))
     with ThreadPoolExecutor(max_workers=len(paths)) as ex:
-        return list(ex.map(_read_matrix, paths))
+        return list(ex.map(read, paths))
+
+
+_POW10F = [float(f"1e{k}") for k in range(309)]
+_FLOAT_RE = re.compile(r"[+-]?(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?")
+_INT_RE = re.compile(r"[+-]?[0-9]{1,15}")
+
+
+def pandas_float(s: str) -> float:
+    """pandas' default float converter for the C parser (precise_xstrtod, the
+    'high' float_precision) on one plain decimal / scientific number: at most
+    17 significant characters of the mantissa are accumulated in double
+    arithmetic (leading zeros count, later integer digits only raise the
+    exponent, later fraction digits are dropped), then the value is scaled by
+    one correctly rounded power of ten (a multiply, or divides below 1e-308).
+    tests/test_cli.py::test_pandas_float_equals_pandas compares it with pandas
+    on 100 000 numbers of many forms."""
+    p, n = 0, len(s)
+    neg = False
+    if p < n and s[p] in "+-":
+        neg = s[p] == "-"
+        p += 1
+    number, exponent, nd, ndec = 0.0, 0, 0, 0
+    while p < n and "0" <= s[p] <= "9":
+        if nd < 17:
+            number = number * 10.0 + (ord(s[p]) - 48)
+            nd += 1
+        else:
+            exponent += 1
+        p += 1
+    if p < n and s[p] == ".":
+        p += 1
+        while nd < 17 and p < n and "0" <= s[p] <= "9":
+            number = number * 10.0 + (ord(s[p]) - 48)
+            p += 1
+            nd += 1
+            ndec += 1
+        while p < n and "0" <= s[p] <= "9":
+            p += 1
+        exponent -= ndec
+    if neg:
+        number = -number
+    if p < n and s[p] in "eE":
+        p += 1
+        eneg = False
+        if p < n and s[p] in "+-":
+            eneg = s[p] == "-"
+            p += 1
+        k = m = 0
+        while k < 17 and p < n and "0" <= s[p] <= "9":
+            m = m * 10 + (ord(s[p]) - 48)
+            k += 1
+            p += 1
+        exponent += -m if eneg else m
+    if exponent > 308:  # pandas flags ERANGE here: left to pandas itself
+        raise ValueError("exponent out of range")
+    if exponent > 0:
+        return number * _POW10F[exponent]
+    if exponent < -308:
+        if exponent < -616:
+            return 0.0 * number
+        return number / _POW10F[-308 - exponent] / _POW10F[308]
+    return number / _POW10F[-exponent]
 
 
 def read_theta(single_group_dir: str, chrom: str) -> np.ndarray:
     """theta_{chrom}.csv.gz, column 'data' (run_inference_two_groups.py:76-79),
-    read by pandas as the reference reads it: pandas' default float converter
-    is not Python's float() (it drops digits past the 17th character of the
-    mantissa, leading zeros included: tests/test_cli.py::test_read_theta_equals_pandas),
-    and theta's bits set every transition probability."""
+    with pandas' values, the reference's reader: pandas' default float
+    converter is not Python's float() (it drops digits past the 17th character
+    of the mantissa, leading zeros included: tests/test_cli.py::
+    test_read_theta_equals_pandas), and theta's bits set every transition
+    probability. A file of the single-group step's form (readr::write_csv of
+    one 'data' column, input_output_functions.R:4-7: a header line, then one
+    plain number per line) is converted here by pandas_float, without
+    importing pandas (half a second of every task); any other text goes to
+    pandas itself."""
+    with gzip.open(os.path.join(single_group_dir, f"theta_{chrom}.csv.gz"), "rt") as fh:
+        lines = fh.read().split("\n")
+    if lines and lines[-1] == "":
+        lines.pop()
+    if len(lines) >= 2 and lines[0] in ("data", '"data"'):
+        vals = lines[1:]
+        if all(_INT_RE.fullmatch(v) for v in vals):  # pandas reads an integer column as int64
+            return np.array([float(int(v)) for v in vals], dtype=np.float64)
+        if all(_FLOAT_RE.fullmatch(v) for v in vals):
+            try:
+                return np.array([pandas_float(v) for v in vals], dtype=np.float64)
+            except ValueError:
+                pass
     import pandas as pd
 
     df = pd.read_table(os.path.join(single_group_dir, f"theta_{chrom}.csv.gz"), sep=",")
@@ -309,7 +491,13 @@ def infer(argv: Sequence[str]) -> int:
 
     LAST_TIMINGS.clear()
     t_parse = time.perf_counter()
-    positions, tot_c, meth_c, tot_k, meth_k = _read_inputs(str(f["data_dir"]), chrom)
+    # The task's rows end at min((batch + 1) * segment + buffer, n): the files are
+    # read that far and no further. segment_index gives the same slice and the
+    # same early exit from the rows read as from the whole chromosome (either
+    # the file holds at least that many rows, or all of it was read), so the
+    # task reads half the chromosome on average instead of all of it.
+    need = (batch + 1) * int(f["segment_size"]) + int(f["buffer_size"])
+    positions, tot_c, meth_c, tot_k, meth_k = _read_inputs(str(f["data_dir"]), chrom, max_rows=max(need, 1))
     LAST_TIMINGS["parse"] = time.perf_counter() - t_parse
 
     seg = segment_index(positions.shape[0], batch, int(f["segment_size"]), int(f["buffer_size"]))
@@ -393,32 +581,55 @@ def _infer_runs(f, mu, sigma, theta, K, T, seed, chrom, batch, ob_c, ob_k, nt_c,
     value (run_inference_two_groups.py:263-322); result writes go to `pool`.
     The chain runs through the host-pointer entry, so this process never needs
     torch: the library is loaded without it (a fresh task saves its import)."""
-    from . import _lib, two_group
+    from . import _lib, serve, two_group
 
-    L = _lib.load(import_torch=False)  # (raises without the HIP library)
-    _use_task_device(L)
-    # tools/bench_pipeline.py: the kernels' own time (HIP events) beside the wall
-    timing = os.environ.get("HYGEIA_TASK_TIMING") == "1"
-    if timing:
-        L.hyg_set_kernel_timing(1)
+    # a running node chain server (`hygeia serve`, serve.py: concurrent tasks'
+    # chains share launches), else this process runs its chain on its device
+    client = serve.task_client()
+    timing = os.environ.get("HYGEIA_TASK_TIMING") == "1"  # tools/bench_pipeline.py: the kernels' own time
+    L = None
 
+    def local():
+        L = _lib.load(import_torch=False)  # (raises without the HIP library)
+        _use_task_device(L)
+        if timing:
+            L.hyg_set_kernel_timing(1)
+        return L
+
+    if client is None:
+        L = local()
     for M in f["num_resampled_particles"]:
         print(M)
         N = int(M) * (2 * K + K * K)
-        model = two_group.CaseControlModel(
-            mu, sigma, theta, minimum_duration=int(f["minimum_duration"]), omega_case=float(f["omega_case"]),
-            merge_log_prob=float(f["merge_log_prob"]), split_prob=float(f["split_prob"]),
-            num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
-            max_total_reads=max_reads, max_duration=T + 1, multinomial=bool(f["multinomial"]))
+        pkw = dict(minimum_duration=int(f["minimum_duration"]), omega_case=float(f["omega_case"]),
+                   merge_log_prob=float(f["merge_log_prob"]), split_prob=float(f["split_prob"]),
+                   num_resampled_ancestors=int(M), num_samples_backward=int(f["num_samples_backward"]),
+                   multinomial=bool(f["multinomial"]))
         t0 = time.time()
-        try:
-            res, _final_w, ex = two_group.run({"control": ob_c, "case": ob_k}, {"control": nt_c, "case": nt_k},
-                                              model, seed, chain_id(chrom, batch))
-        finally:
-            model.close()
+        res = None
+        if client is not None:
+            try:
+                res, _final_w, ex = client.run_chain(_lib.make_params(mu, sigma, theta, **pkw), max_reads,
+                                                     ob_c, nt_c, ob_k, nt_k, seed, chain_id(chrom, batch))
+                LAST_TIMINGS["server_batch"] = client.last.get("batch", 0)
+                LAST_TIMINGS["server_wait"] = client.last.get("wait_s", 0.0)
+                LAST_TIMINGS["kernels"] = LAST_TIMINGS.get("kernels", 0.0) + client.last.get("run_s", 0.0)
+            except serve.ServerUnavailable as e:
+                print(f"hygeia: chain server unavailable ({e}); running the chain in this process", file=sys.stderr)
+                client, res = None, None
+                L = local()
+                t0 = time.time()
+        if res is None:
+            model = two_group.CaseControlModel(mu, sigma, theta, max_total_reads=max_reads, max_duration=T + 1,
+                                               **pkw)
+            try:
+                res, _final_w, ex = two_group.run({"control": ob_c, "case": ob_k}, {"control": nt_c, "case": nt_k},
+                                                  model, seed, chain_id(chrom, batch))
+            finally:
+                model.close()
         times[N] = time.time() - t0
         LAST_TIMINGS["chains"] = LAST_TIMINGS.get("chains", 0.0) + times[N]  # (inside "device")
-        if timing:
+        if timing and L is not None:
             import ctypes as C
 
             ms3 = (C.c_float * 3)()
@@ -641,6 +852,9 @@ def main(argv: Sequence[str] = None) -> int:
         except FlagError as e:
             print(f"Error: {e}", file=sys.stderr)
             return 1
+    if cmd == "serve":  # the operator-run node chain server for concurrent `infer` tasks (serve.py)
+        from . import serve
+        return serve.main(rest)
     if cmd in ("version", "-v", "--version"):
         # every 4_infer.nf task runs this for versions.yml (:54-57): no torch
         # import, no HIP library load (_lib.VERSION equals hyg_version())
@@ -652,6 +866,7 @@ def main(argv: Sequence[str] = None) -> int:
               "  get_chrom_segments - Get chromosome segments\n"
               "  infer     - Run inference on two groups (MI355X)\n"
               "  infer_many - Every (batch, seed) task of a chromosome in one launch (MI355X)\n"
+              "  serve     - Node chain server: concurrent infer tasks share launches (MI355X)\n"
               "  aggregate - Aggregate results\n  get_dmps  - Get DMPs (Differentially Methylated Positions)\n"
               "  make_bed_file - Regime BED track of a single-group regimes CSV (MI355X)\n"
               "  estimate_parameters_and_regimes - Single-group regimes and parameters (MI355X)")

@@ -5,6 +5,7 @@ flags (:19-72), segment slicing and early exit (:194-218), file layout (:101-108
 import gzip
 import math
 import os
+import time
 
 import numpy as np
 import pytest
@@ -283,3 +284,124 @@ def test_single_task_does_not_import_torch(tmp_path):
     r = subprocess.run([sys.executable, "-c", code] + args, capture_output=True, text=True, cwd=root,
                        env=dict(os.environ, PYTHONPATH=root), timeout=300)
     assert "torch imported: False" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("fmt", ["%d", "%.18e", "%.1f"])
+def test_partial_read_equals_whole_file_prefix(tmp_path, fmt):
+    """A task reads its count files only up to its last row
+    ((batch + 1) * segment + buffer): the rows read equal the whole file's
+    first rows, across the streaming reader's blocks and at the end of the
+    file, for the pipeline's number formats; a non-integral value falls back to
+    pandas (nrows) with the same result."""
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 400, (130_000, 4)).astype(np.float64)
+    p = str(tmp_path / "m.txt.gz")
+    np.savetxt(p, a, fmt=fmt, delimiter=",")
+    whole = cli._read_matrix(p)
+    np.testing.assert_array_equal(whole, a)
+    for n in (1, 999, 65_536, 100_001, 129_999, 130_000, 130_001, 10 ** 9):
+        got = cli._read_matrix(p, max_rows=n)
+        np.testing.assert_array_equal(got, a[:n])
+    b = a.copy()
+    b[5, 1] = 0.5  # not a count: the pandas path
+    q = str(tmp_path / "f.txt.gz")
+    np.savetxt(q, b, fmt="%.18e", delimiter=",")
+    np.testing.assert_array_equal(cli._read_matrix(q, max_rows=70_000), b[:70_000])
+
+
+def test_segment_of_partial_read_equals_whole(tmp_path):
+    """segment_index on the rows a task reads gives the slice and the early exit
+    it gives on the whole chromosome, for every batch."""
+    for n in (1, 999, 1000, 1001, 2600, 5000):
+        for b in range(0, n // 1000 + 3):
+            need = (b + 1) * 1000 + 60
+            assert cli.segment_index(min(n, max(need, 1)), b, 1000, 60) == cli.segment_index(n, b, 1000, 60)
+
+
+def test_version_answer_of_the_wrapper_equals_the_cli(capsys):
+    """bin/hygeia answers --version itself (every 4_infer.nf task runs it); the
+    text equals hygeia_amd.cli's, which equals the library's hyg_version()
+    (tests/test_capi_cpu.py)."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for arg in ("--version", "-v", "version"):
+        env = dict(os.environ, HYGEIA_VERSION="9.9")
+        out = subprocess.run([os.path.join(root, "bin", "hygeia"), arg], capture_output=True, text=True, env=env)
+        assert out.returncode == 0
+        os.environ["HYGEIA_VERSION"] = "9.9"
+        try:
+            assert cli.main([arg]) == 0
+        finally:
+            del os.environ["HYGEIA_VERSION"]
+        assert out.stdout == capsys.readouterr().out == "Hygeia version 9.9 (hygeia_amd 0.1.0 (gfx950))\n"
+
+
+def test_pandas_float_equals_pandas():
+    """cli.pandas_float (read_theta's converter) against pandas' C parser on
+    100 000 numbers: repr, %.18e, %.17g, 25-decimal fixed, long fractions with
+    leading zeros, many-digit integers and fractions; bit for bit."""
+    import io
+
+    import pandas as pd
+
+    rng = np.random.default_rng(1)
+    strs = []
+    for i in range(100_000):
+        x = float(rng.normal() * 10.0 ** rng.integers(-30, 30))
+        f = i % 6
+        if f == 0:
+            s = repr(x)
+        elif f == 1:
+            s = "%.18e" % x
+        elif f == 2:
+            s = "%.17g" % x
+        elif f == 3:
+            s = "%.25f" % x if abs(x) < 1e5 else repr(x)
+        elif f == 4:
+            s = "0.000" + str(rng.integers(0, 10 ** 18))
+        else:
+            s = str(rng.integers(-10 ** 6, 10 ** 6)) + "." + str(rng.integers(0, 10 ** 12)).zfill(12)
+        strs.append(s)
+    want = pd.to_numeric(pd.read_table(io.StringIO("data\n" + "\n".join(strs) + "\n"), sep=",")["data"]).to_numpy(
+        dtype=np.float64)
+    got = np.array([cli.pandas_float(s) for s in strs])
+    assert np.array_equal(got.view(np.int64), want.view(np.int64))
+    assert not np.array_equal(got, np.array([float(s) for s in strs]))  # not Python's float()
+
+
+def test_parse_cache(tmp_path):
+    """The parse cache returns the parse's values (int32-stored counts, float64
+    positions beyond int32, a float matrix kept as float64), is filled once under
+    concurrent readers, follows a rewritten file, and is placed by
+    parse_cache_dir (env, Nextflow workDir, or off)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 500, (20_000, 3)).astype(np.float64)
+    big = (rng.integers(0, 2 ** 40, (3000, 1))).astype(np.float64)
+    p, q = str(tmp_path / "a.txt.gz"), str(tmp_path / "b.txt.gz")
+    np.savetxt(p, a, fmt="%.18e", delimiter=",")
+    np.savetxt(q, big, fmt="%d", delimiter=",")
+    cache = str(tmp_path / "cache")
+    with ThreadPoolExecutor(8) as ex:
+        outs = list(ex.map(lambda n: cli._cached_matrix(p, cache, n), [None, 5, 19_999, 20_000, 10 ** 6] * 4))
+    for o, n in zip(outs, [None, 5, 19_999, 20_000, 10 ** 6] * 4):
+        assert o.dtype == np.float64
+        np.testing.assert_array_equal(o, a if n is None else a[:n])
+    npys = [f for f in os.listdir(cache) if f.endswith(".npy")]
+    assert len(npys) == 1 and np.load(os.path.join(cache, npys[0])).dtype == np.int32
+    np.testing.assert_array_equal(cli._cached_matrix(q, cache, 100), big[:100])
+    assert sorted(np.load(os.path.join(cache, f)).dtype.str for f in os.listdir(cache) if f.endswith(".npy")) == [
+        "<f8", "<i4"]
+    time.sleep(0.01)
+    np.savetxt(p, a[:7] + 1, fmt="%d", delimiter=",")  # rewritten: a new key
+    np.testing.assert_array_equal(cli._cached_matrix(p, cache), a[:7] + 1)
+    # where it lives
+    assert cli.parse_cache_dir({"HYGEIA_PARSE_CACHE": "/x"}) == "/x"
+    assert cli.parse_cache_dir({"HYGEIA_PARSE_CACHE": "0"}, cwd=str(tmp_path)) is None
+    assert cli.parse_cache_dir({}, cwd=str(tmp_path)) is None
+    task = tmp_path / "work" / "ab" / "cdef"
+    task.mkdir(parents=True)
+    (task / ".command.sh").write_text("hygeia infer\n")
+    assert cli.parse_cache_dir({}, cwd=str(task)) == str(tmp_path / "work" / ".hygeia_parse_cache")

@@ -22,7 +22,11 @@ way Nextflow's local executor runs the module's fan-out on a node
 the per-task wall times; `infer_many` runs as a subprocess too, so the parent
 never holds a GPU context (the GPU box admits at most 16 processes on its card,
 which caps N there).
+--server (round 6) runs the --concurrent tasks through the node chain server
+(`hygeia serve`, hygeia_amd/serve.py), started before the sweep and stopped
+after it: the tasks are unchanged processes; their chains share launches.
 usage: python tools/bench_pipeline.py [--sites N] [--seeds 0,1] [--workdir DIR] [--concurrent LIST]
+                                      [--server [--gather S]] [--task-env K=V]
 """
 from __future__ import annotations
 
@@ -104,6 +108,9 @@ def concurrent_sweep(wd, common, seeds, sites, n_batches, ns, env=None):
     out = []
     for n in ns:
         rdir = os.path.join(wd, f"conc{n}")
+        pc = (env or {}).get("HYGEIA_PARSE_CACHE", "0")
+        if pc != "0":  # every N starts with an empty parse cache (a fresh pipeline run)
+            shutil.rmtree(pc, ignore_errors=True)
 
         def one(t):
             b, sd = t
@@ -118,6 +125,8 @@ def concurrent_sweep(wd, common, seeds, sites, n_batches, ns, env=None):
         wall = time.perf_counter() - t0
         walls = np.array([r["wall_s"] for r in res])
         chains = np.array([r["split"].get("chains", 0.0) for r in res])
+        keys = sorted({k for r in res for k, v in r["split"].items() if isinstance(v, (int, float))} - {"rc", "slot"})
+        split_mean = {k: float(np.mean([r["split"].get(k, 0.0) for r in res])) for k in keys}
         kern = np.array([r["split"].get("kernels", 0.0) for r in res])
         ver = np.array([r["split"].get("version", 0.0) for r in res])
         rec = {"concurrent": n, "tasks": len(tasks), "wall_s": wall, "value": units / wall,
@@ -125,6 +134,7 @@ def concurrent_sweep(wd, common, seeds, sites, n_batches, ns, env=None):
                "task_chains_s": {"mean": float(chains.mean()), "max": float(chains.max())},
                "task_kernels_s": {"mean": float(kern.mean()), "max": float(kern.max())},
                "task_version_s": {"mean": float(ver.mean()), "max": float(ver.max())},
+               "task_split_mean_s": split_mean,
                "devices": sorted({(r["split"]["device"], r["split"]["slot"]) for r in res})}
         out.append(rec)
         print(json.dumps(rec), flush=True)
@@ -140,6 +150,11 @@ def main():
     ap.add_argument("--concurrent", default="", help="comma list of N: every task as a process, N at once")
     ap.add_argument("--task-env", action="append", default=[], metavar="KEY=VALUE",
                     help="extra environment of the task processes (e.g. GPU_MAX_HW_QUEUES=1)")
+    ap.add_argument("--server", action="store_true",
+                    help="--concurrent through the node chain server (`hygeia serve`, started and stopped here)")
+    ap.add_argument("--gather", type=float, default=0.0, help="the server's gather window (s)")
+    ap.add_argument("--parse-cache", action="store_true",
+                    help="--concurrent tasks share a parse cache (HYGEIA_PARSE_CACHE, as inside a Nextflow run)")
     a = ap.parse_args()
     if a.concurrent:
         return main_concurrent(a)
@@ -210,11 +225,39 @@ def main_concurrent(a):
     print(f"infer_many {many['wall_s']:.1f} s", flush=True)
     env = dict(os.environ)
     env.update(kv.split("=", 1) for kv in a.task_env)
-    sweep = concurrent_sweep(wd, common, seeds, a.sites, n_batches, [int(x) for x in a.concurrent.split(",")], env)
+    env.setdefault("HYGEIA_PARSE_CACHE", os.path.join(wd, "parse_cache") if a.parse_cache else "0")
+    srv, server_status = None, None
+    if a.server:  # the node chain server (`hygeia serve`), started and stopped here
+        from hygeia_amd import serve
+
+        lockd = os.path.join(wd, "locks")
+        os.makedirs(lockd, exist_ok=True)
+        env["HYGEIA_DEVICE_LOCK_DIR"] = lockd
+        path = serve.socket_path(lockd)
+        srv = subprocess.Popen([sys.executable, "-m", "hygeia_amd.serve", "--socket", path, "--gather",
+                                str(a.gather)], env=dict(env, PYTHONPATH=ROOT), cwd=ROOT)
+        t0 = time.perf_counter()
+        while not serve.connectable(path):
+            if srv.poll() is not None or time.perf_counter() - t0 > 120:
+                raise RuntimeError("the chain server did not start")
+            time.sleep(0.1)
+        print(f"server up in {time.perf_counter() - t0:.1f} s", flush=True)
+    try:
+        sweep = concurrent_sweep(wd, common, seeds, a.sites, n_batches, [int(x) for x in a.concurrent.split(",")],
+                                 env)
+        if srv is not None:
+            server_status = serve.Client(path).status()
+            serve.Client(path).stop()
+            srv.wait(timeout=300)
+    finally:
+        if srv is not None and srv.poll() is None:
+            srv.kill()
+            srv.wait()
     line = {"metric": "pipeline CpG sites x seeds / s (hygeia infer, gz CSV in -> result files out)",
             "sites": a.sites, "seeds": seeds, "tasks": n_batches * len(seeds),
             "infer_many": {"value": units / many["wall_s"], "wall_s": many["wall_s"], "split_s": many["split"]},
-            "concurrent_tasks": sweep, "task_env": a.task_env,
+            "concurrent_tasks": sweep, "task_env": a.task_env, "parse_cache": a.parse_cache,
+            "server": ({"gather_s": a.gather, "status": server_status} if a.server else None),
             "note": "each task a fresh `hygeia infer` process, N at once on one GPU (Nextflow local executor)"}
     print(json.dumps(line), flush=True)
     if a.workdir is None:
