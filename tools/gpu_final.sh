@@ -52,6 +52,8 @@ step bench_c2 600 python tools/bench_sg.py
 step bench_c1 600 python tools/bench_sg.py --config c1
 step bench_pipe 600 python tools/bench_pipeline.py
 step bench_pipe_concurrent 600 python tools/bench_pipeline.py --concurrent 8,16
+step bench_pipe_concurrent_cache 600 python tools/bench_pipeline.py --concurrent 16 --parse-cache
+step bench_pipe_concurrent_server 600 python tools/bench_pipeline.py --concurrent 16 --parse-cache --server --gather 0.5
 fi
 rc=0
 if [ "${2:-}" != "no-profile" ] && [ "$part" = "all" ]; then  # (the profile set can run as its own call: bash tools/gpu_profile.sh <tag>)
