@@ -46,6 +46,7 @@ MODE_VAR = "HYGEIA_SERVER"  # "0": tasks ignore a running server
 SOCK_NAME = "hygeia_amd.server.sock"
 IDLE_S = 0.0  # 0: run until stopped
 MAX_HEADER = 1 << 20
+SERVER_FAULT = 1  # reply code of a failure of the server itself (not of the chain): the task runs the chain itself
 
 
 class ServerUnavailable(RuntimeError):
@@ -141,9 +142,10 @@ class Client:
                 "s_c": int(tc.shape[1]), "s_k": int(tk.shape[1]), "seed": int(seed), "chain_id": int(chain_id)}
         h, bufs = self._call(head, (mc, tc, mk, tk))
         self.last = h
-        if h.get("rc", -1) != 0:
-            if h.get("rc") in _lib.ERROR_NAMES:
-                raise _lib.HygError(int(h["rc"]), h.get("error", ""))
+        rc = h.get("rc", SERVER_FAULT)
+        if rc != 0:
+            if rc in _lib.ERROR_NAMES:  # the chain's own failure, as the library reports it in-process
+                raise _lib.HygError(int(rc), h.get("error", ""))
             raise ServerUnavailable(h.get("error", "server error"))
         K, B = int(params.n_regimes), int(params.num_samples_backward)
         merged = np.frombuffer(bufs[0], np.int16).reshape(T, B)
@@ -180,7 +182,7 @@ class _Request:
     def __init__(self, header, bufs):
         self.header, self.bufs = header, bufs
         self.done = threading.Event()
-        self.reply: Tuple[dict, list] = ({"rc": -1, "error": "not run"}, [])
+        self.reply: Tuple[dict, list] = ({"rc": SERVER_FAULT, "error": "not run"}, [])
         self.t_in = time.monotonic()
 
     def key(self):
@@ -326,7 +328,7 @@ class Server:
                 eng.run(batch)
             except Exception as e:
                 for r in batch:
-                    r.reply = ({"rc": -3, "error": f"server: {e}"}, [])
+                    r.reply = ({"rc": SERVER_FAULT, "error": f"server: {e}"}, [])
             with self.cv:
                 self.busy -= 1
                 self.last_work = time.monotonic()
@@ -358,7 +360,7 @@ class Server:
                     r = _Request(header, bufs)
                     with self.cv:
                         if self.stopping:
-                            send_msg(conn, {"rc": -3, "error": "server stopping"})
+                            send_msg(conn, {"rc": SERVER_FAULT, "error": "server stopping"})
                             return
                         self.stats["requests"] += 1
                         self.pending.append(r)
@@ -366,10 +368,10 @@ class Server:
                     r.done.wait()
                     send_msg(conn, *r.reply)
                 else:
-                    send_msg(conn, {"rc": -1, "error": f"unknown op {op!r}"})
+                    send_msg(conn, {"rc": SERVER_FAULT, "error": f"unknown op {op!r}"})
             except (OSError, ValueError, KeyError) as e:
                 try:
-                    send_msg(conn, {"rc": -1, "error": f"bad request: {e}"})
+                    send_msg(conn, {"rc": SERVER_FAULT, "error": f"bad request: {e}"})
                 except OSError:
                     pass
 
@@ -405,6 +407,11 @@ class Server:
         finally:
             for w in workers:
                 w.join(timeout=600)
+            with self.cv:  # requests no worker took (every device failed): their tasks run them
+                left, self.pending = self.pending, []
+            for r in left:
+                r.reply = ({"rc": SERVER_FAULT, "error": "server: no usable device"}, [])
+                r.done.set()
             srv.close()
             try:
                 if os.stat(self.path).st_ino == ino:

@@ -187,3 +187,63 @@ def test_infer_writes_the_server_replies(fake_server, tmp_path, monkeypatch):
     v = (tc.sum(1).astype(np.int64) + 2 + (cli.chain_id("3", 0) & 0xFFFF)) % 1000
     np.testing.assert_array_equal(merged[:, 0], v)
     assert (d / "log_normalizing_constants_optimal_2.txt").read_text().strip() == str({2400: float(v.sum())})
+
+
+class FailingEngine(FakeEngine):
+    """Chains whose seed is 13 fail as the library would (all weights -inf);
+    seed 99 makes the engine itself raise (a server fault)."""
+
+    def run(self, reqs):
+        if any(r.header["seed"] == 99 for r in reqs):
+            raise RuntimeError("device lost")
+        super().run(reqs)
+        for r in reqs:
+            if r.header["seed"] == 13:
+                r.reply = ({"rc": _lib.HYG_ENUMERIC, "error": "all particle weights became -inf"}, [])
+
+
+def test_chain_errors_and_server_faults(tmp_path):
+    """A chain's own failure reaches the task as the library's error (as if it
+    had run in-process); a failure of the server reaches it as
+    ServerUnavailable, on which `hygeia infer` runs the chain itself; so does a
+    connection the server drops."""
+    path = str(tmp_path / "f.sock")
+    srv = serve.Server(path, 1, engine_factory=FailingEngine, idle=30)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    t0 = time.monotonic()
+    while not serve.connectable(path):
+        assert time.monotonic() - t0 < 10
+        time.sleep(0.02)
+    try:
+        p, mc, tc, mk, tk, _ = _req(40, 2, 0)
+        c = serve.Client(path)
+        with pytest.raises(_lib.HygError) as ei:
+            c.run_chain(p, 60, mc, tc, mk, tk, 13, 1)
+        assert ei.value.code == _lib.HYG_ENUMERIC
+        with pytest.raises(serve.ServerUnavailable, match="device lost"):
+            c.run_chain(p, 60, mc, tc, mk, tk, 99, 1)
+        c.run_chain(p, 60, mc, tc, mk, tk, 1, 1)  # the server still serves
+    finally:
+        serve.Client(path).stop()
+        th.join(timeout=30)
+    # a listener that drops every connection
+    dead = str(tmp_path / "d.sock")
+    ls = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    ls.bind(dead)
+    ls.listen(4)
+
+    def drop():
+        for _ in range(2):
+            conn, _ = ls.accept()
+            conn.close()
+
+    dt = threading.Thread(target=drop, daemon=True)
+    dt.start()
+    try:
+        assert not serve.connectable(dead)
+        with pytest.raises(serve.ServerUnavailable):
+            serve.Client(dead).run_chain(p, 60, mc, tc, mk, tk, 1, 1)
+    finally:
+        dt.join(timeout=10)
+        ls.close()
