@@ -220,6 +220,9 @@ class Engine:
         p = _lib.TgParams.from_buffer_copy(bytes.fromhex(params_hex))
         h = C.c_void_p()
         _lib.check(self.L.hyg_tg_model_create(C.byref(p), int(reads), int(sites), C.byref(h)))
+        if len(self.models) >= 8:  # the oldest parameter set's model goes
+            old = next(iter(self.models))
+            self.L.hyg_tg_model_destroy(self.models.pop(old)[0])
         self.models[params_hex] = (h, reads, sites)
         return h
 
@@ -259,8 +262,8 @@ class Engine:
         off = 0
         for i, r in enumerate(reqs):
             T = Ts[i]
-            if rc:
-                r.reply = ({"rc": int(rc), "error": err}, [])
+            if rc:  # the launch failed (e.g. the batch's memory): each task runs its chain itself
+                r.reply = ({"rc": SERVER_FAULT, "error": f"server launch: {err}"}, [])
             elif status[i] != 0:
                 r.reply = ({"rc": int(status[i]), "error": "all particle weights became -inf"}, [])
             else:
@@ -278,7 +281,7 @@ class Server:
     (tests pass a fake one)."""
 
     def __init__(self, path: str, n_devices: int, engine_factory=Engine, idle: float = IDLE_S,
-                 max_batch_sites: int = 64_000_000, gather: float = 0.0):
+                 max_batch_sites: int = 16_000_000, gather: float = 0.0):
         self.path, self.idle, self.max_batch_sites = path, float(idle), int(max_batch_sites)
         self.gather = float(gather)  # seconds a free device waits after the oldest request for more to join
         self.pending: List[_Request] = []
