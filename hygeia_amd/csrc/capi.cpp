@@ -153,7 +153,7 @@ struct hyg_tg_model {
   int32_t dcap = 0;
   int32_t nmax_reads = 0;
   int32_t max_duration = 0;
-  std::vector<double> hz, lf, lg, cst;
+  std::vector<double> hz, lf, lg, cst, bbt;
   bool on_device = false;
   int device = -1;
   hyg_tg_consts* d_consts = nullptr;
@@ -161,6 +161,7 @@ struct hyg_tg_model {
   double* d_lf = nullptr;
   double* d_lg = nullptr;
   double* d_cst = nullptr;
+  double* d_bbt = nullptr;
   mutable PinnedStages stage;  // descriptor uploads (thread-safe, one pinned buffer per stream)
 
   ModelDev dev() const {
@@ -172,9 +173,15 @@ struct hyg_tg_model {
     m.lf = d_lf;
     m.lg = d_lg;
     m.cst = d_cst;
+    m.bbt = d_bbt;
     return m;
   }
 };
+
+// The emission's per-(n, y) term table is built when it stays L2-sized (the
+// pipeline's coverage: max reads ~170, 0.7 MB at K = 6); beyond that the
+// emission forms each term from the lgamma rows.
+constexpr size_t kBbtMaxBytes = (size_t)16 << 20;
 
 struct hyg_sg_model {
   hyg_sg_consts c{};
@@ -316,6 +323,7 @@ void hyg_tg_model_destroy(hyg_tg_model* m) {
     (void)hipFree(m->d_lf);
     (void)hipFree(m->d_lg);
     (void)hipFree(m->d_cst);
+    (void)hipFree(m->d_bbt);
   }
   delete m;
 }
@@ -342,6 +350,10 @@ int hyg_tg_model_create(const hyg_tg_params* params, int32_t max_total_reads, in
   m->lg.resize((size_t)3 * K * L);
   m->cst.resize(K);
   hyg_bb_tables(&m->c, max_total_reads, m->lf.data(), m->lg.data(), m->cst.data());
+  if (hyg_bb_term_table_len(K, max_total_reads) * sizeof(double) <= kBbtMaxBytes) {
+    m->bbt.resize(hyg_bb_term_table_len(K, max_total_reads));
+    hyg_bb_term_table(K, max_total_reads, m->lf.data(), m->lg.data(), m->cst.data(), m->bbt.data());
+  }
   if (have_device()) {
     (void)hipGetDevice(&m->device);
     hipError_t e = hipSuccess;
@@ -350,6 +362,7 @@ int hyg_tg_model_create(const hyg_tg_params* params, int32_t max_total_reads, in
     if (e == hipSuccess) e = dmalloc_copy(&m->d_lf, m->lf.data(), m->lf.size());
     if (e == hipSuccess) e = dmalloc_copy(&m->d_lg, m->lg.data(), m->lg.size());
     if (e == hipSuccess) e = dmalloc_copy(&m->d_cst, m->cst.data(), m->cst.size());
+    if (e == hipSuccess && !m->bbt.empty()) e = dmalloc_copy(&m->d_bbt, m->bbt.data(), m->bbt.size());
     m->on_device = true;
     if (e != hipSuccess) {
       hyg_tg_model_destroy(m);

@@ -60,6 +60,7 @@ struct ModelDev {
   const double* lf;   // [nmax+1]
   const double* lg;   // [K][3][nmax+1]
   const double* cst;  // [K]
+  const double* bbt;  // per-(n, y) terms [(nmax+1)(nmax+2)/2][K] (hyg_bb_term_table), or null when too large
 };
 
 struct FwdLayout {  // LDS carve of the forward kernel (byte offsets)

@@ -1610,6 +1610,103 @@ tg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
   }
 }
 
+// The same sums from the per-(n, y) term table (hyg_bb_term_table: every
+// regime's term of a sample in one row of K doubles, built with the per-term
+// kernel's operations, so each entry has the bits that kernel forms): one row
+// load per sample instead of 3 + 3K table gathers. The table is L2-sized at
+// the pipeline's coverage (0.7 MB at K = 6), so the kernel streams the counts
+// in and the rows out at close to the HBM rate. KT > 0: the regime count at
+// compile time (rows as 16-byte loads).
+template <int KT>
+__global__ void __launch_bounds__(kETile)
+tg_emission_tab_kernel(const double* __restrict__ bbt, int L, int Kr, const uint16_t* __restrict__ meth_c,
+                       const uint16_t* __restrict__ tot_c, int s_c, const uint16_t* __restrict__ meth_k,
+                       const uint16_t* __restrict__ tot_k, int s_k, int64_t T, double* __restrict__ E) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* tile = (double*)smem;  // [kETile][2K]
+  const int K = KT ? KT : Kr, K2 = 2 * K;
+  for (int64_t t0 = (int64_t)blockIdx.x * kETile; t0 < T; t0 += (int64_t)gridDim.x * kETile) {
+    const int64_t t = t0 + threadIdx.x;
+    if (t < T) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int S = g ? s_k : s_c;
+        const uint16_t* my = g ? meth_k + t * s_k : meth_c + t * s_c;
+        const uint16_t* nt = g ? tot_k + t * s_k : tot_c + t * s_c;
+        double e[KT ? KT : HYG_KMAX];
+#pragma unroll
+        for (int r = 0; r < (KT ? KT : HYG_KMAX); ++r) e[r] = 0.0;
+        bool bad = false;
+        // samples in chunks of kCh: every count load of the chunk issued first,
+        // then every row load, then the sums in sample order (a sample with
+        // n = 0 adds nothing, as the per-term kernel skips it)
+        constexpr int kCh = 4;
+        // (an even sample count with 4-byte aligned rows: the counts as pairs)
+        const bool pairs = (S % 2 == 0) && ((((uintptr_t)my) | ((uintptr_t)nt)) & 3) == 0;
+        for (int s0 = 0; s0 < S; s0 += kCh) {
+          int nn[kCh], yy[kCh];
+          if (pairs) {
+#pragma unroll
+            for (int j = 0; j < kCh; j += 2) {
+              const int sj = s0 + j < S ? s0 + j : S - 2;
+              const uint32_t a = *(const uint32_t*)(nt + sj), b = *(const uint32_t*)(my + sj);
+              nn[j] = (int)(a & 0xffffu);
+              nn[j + 1] = (int)(a >> 16);
+              yy[j] = (int)(b & 0xffffu);
+              yy[j + 1] = (int)(b >> 16);
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < kCh; ++j) {
+              const int sj = s0 + j < S ? s0 + j : S - 1;
+              nn[j] = nt[sj];
+              yy[j] = my[sj];
+            }
+          }
+          size_t off[kCh];
+          bool use[kCh];
+#pragma unroll
+          for (int j = 0; j < kCh; ++j) {
+            const int n = nn[j], y = yy[j];
+            use[j] = s0 + j < S && n != 0;
+            bad = bad || (use[j] && (y > n || n >= L));  // invalid input: poison the row
+            use[j] = use[j] && y <= n && n < L;
+            off[j] = use[j] ? ((size_t)n * (size_t)(n + 1) / 2 + (size_t)y) * (size_t)K : 0;
+          }
+          if constexpr (KT > 0 && KT % 2 == 0) {
+            double2 v[kCh][KT / 2];
+#pragma unroll
+            for (int j = 0; j < kCh; ++j)
+#pragma unroll
+              for (int r = 0; r < KT / 2; ++r) v[j][r] = *(const double2*)(bbt + off[j] + 2 * r);
+#pragma unroll
+            for (int j = 0; j < kCh; ++j)
+#pragma unroll
+              for (int r = 0; r < KT / 2; ++r) {
+                e[2 * r] = use[j] ? e[2 * r] + v[j][r].x : e[2 * r];
+                e[2 * r + 1] = use[j] ? e[2 * r + 1] + v[j][r].y : e[2 * r + 1];
+              }
+          } else {
+#pragma unroll
+            for (int j = 0; j < kCh; ++j)
+              if (use[j])
+                for (int r = 0; r < K; ++r) e[r] = e[r] + bbt[off[j] + r];
+          }
+        }
+        for (int r = 0; r < K; ++r) tile[threadIdx.x * K2 + g * K + r] = bad ? HYG_NAN : e[r];
+      }
+    }
+    __syncthreads();
+    const int64_t rows = (T - t0) < kETile ? (T - t0) : kETile;
+    const int n = (int)rows * K2;
+    double* dst = E + t0 * K2;
+    for (int i = 2 * threadIdx.x; i + 1 < n; i += 2 * kETile)
+      *(double2*)(dst + i) = make_double2(tile[i], tile[i + 1]);
+    if ((n & 1) && threadIdx.x == 0) dst[n - 1] = tile[n - 1];
+    __syncthreads();
+  }
+}
+
 // Three waves per SIMD (<= 168 VGPRs) at 256 and 768 threads: a CU holds three
 // chains or one (the second argument is the minimum waves per SIMD); 512
 // threads (one chain per CU: C5 by its LDS, or a low-occupancy launch) may use
@@ -2847,8 +2944,20 @@ int launch_emission(const ModelDev& md, const hyg_tg_consts& c, const uint16_t* 
   if (blocks > 256 * 16) blocks = 256 * 16;
   ev_record(0, false, (hipStream_t)stream);
   const size_t lds = sizeof(double) * kETile * 2 * c.K;
-  hipLaunchKernelGGL(tg_emission_kernel, dim3((unsigned)blocks), dim3(kETile), lds, (hipStream_t)stream, md.lf,
-                     md.lg, md.cst, md.nmax_reads + 1, c.K, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E);
+  const int L = md.nmax_reads + 1;
+  if (md.bbt && c.K == 6) {
+    hipLaunchKernelGGL(tg_emission_tab_kernel<6>, dim3((unsigned)blocks), dim3(kETile), lds, (hipStream_t)stream,
+                       md.bbt, L, c.K, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E);
+  } else if (md.bbt && c.K == 12) {
+    hipLaunchKernelGGL(tg_emission_tab_kernel<12>, dim3((unsigned)blocks), dim3(kETile), lds, (hipStream_t)stream,
+                       md.bbt, L, c.K, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E);
+  } else if (md.bbt) {
+    hipLaunchKernelGGL(tg_emission_tab_kernel<0>, dim3((unsigned)blocks), dim3(kETile), lds, (hipStream_t)stream,
+                       md.bbt, L, c.K, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E);
+  } else {
+    hipLaunchKernelGGL(tg_emission_kernel, dim3((unsigned)blocks), dim3(kETile), lds, (hipStream_t)stream, md.lf,
+                       md.lg, md.cst, L, c.K, meth_c, tot_c, s_c, meth_k, tot_k, s_k, n_sites, E);
+  }
   ev_record(0, true, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? HYG_OK : HYG_EDEVICE;
 }

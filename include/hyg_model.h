@@ -256,4 +256,32 @@ static inline void hyg_bb_tables(const hyg_tg_consts* c, int nmax, double* lf, d
   }
 }
 
+/* The per-(n, y) Beta-Binomial terms of every regime, from the tables above:
+ * bbt[(n (n + 1) / 2 + y) K + r] = log BB(y | n, alpha_r, beta_r) for
+ * 0 <= y <= n <= nmax, formed with exactly the operations and order of the
+ * emission's per-sample term (tg_emission_kernel), so a sum of table entries
+ * over the samples has the bits of the per-term sum. (nmax + 1)(nmax + 2) / 2
+ * K doubles. */
+static inline size_t hyg_bb_term_table_len(int K, int nmax) {
+  return (size_t)(nmax + 1) * (size_t)(nmax + 2) / 2 * (size_t)K;
+}
+static inline void hyg_bb_term_table(int K, int nmax, const double* lf, const double* lg, const double* cst,
+                                     double* bbt) {
+  const int L = nmax + 1;
+  for (int n = 0; n < L; ++n) {
+    for (int y = 0; y <= n; ++y) {
+      double base = lf[n] - lf[y];
+      base = base - lf[n - y];
+      double* row = bbt + ((size_t)n * (size_t)(n + 1) / 2 + (size_t)y) * (size_t)K;
+      for (int r = 0; r < K; ++r) {
+        double term = base + lg[(size_t)(r * 3 + 0) * L + y];
+        term = term + lg[(size_t)(r * 3 + 1) * L + (n - y)];
+        term = term - lg[(size_t)(r * 3 + 2) * L + n];
+        term = term + cst[r];
+        row[r] = term;
+      }
+    }
+  }
+}
+
 #endif /* HYG_MODEL_H */

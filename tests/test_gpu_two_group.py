@@ -443,3 +443,35 @@ def test_tail_overlap_equals_one_launch(oracle):
         assert a["log_z"][i] == ref["log_z"]
         np.testing.assert_array_equal(a["final_w"][i], ref["final_log_weights"])
 
+
+
+@pytest.mark.parametrize("K,S", [(6, 4), (12, 50), (4, 3)])
+def test_emission_table_equals_per_term_path(oracle, K, S):
+    """The emission from the per-(n, y) term table (built at model creation
+    when it stays L2-sized) has the bits of the per-term emission (a model
+    whose read range makes the table too large) and of the oracle, at the
+    pipeline shape, the stress shape (K = 12, 50 samples) and a generic K; zero
+    coverage and invalid rows included."""
+    from hygeia_amd import two_group
+
+    T = 6000
+    mu, sg, theta, d, p = _setup(oracle, K, 50, 25, T, S, 100.0, 40 + K)
+    for k in ("meth_control", "tot_control", "meth_case", "tot_case"):
+        d[k][100:130] = 0
+    d["meth_case"][200, 0] = d["tot_case"][200, 0] + 1  # methylated > total: a NaN row on every path
+    maxr = int(max(d["tot_control"].max(), d["tot_case"].max()))
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(d[k]).view(np.int16)).to(dev) for k in
+         ("meth_control", "tot_control", "meth_case", "tot_case")}
+    out = []
+    for reads in (maxr, 3000):  # (3000: a table of 144-864 MB, over the 16 MB bound: the per-term kernel)
+        m = _model(mu, sg, theta, 50, 25, reads, 10)
+        dc = two_group.DeviceChains(m, [(0, 5, 0, 0, 0)], 5, device=dev)
+        out.append(dc.emission(t["meth_control"], t["tot_control"], t["meth_case"], t["tot_case"]).cpu().numpy())
+    np.testing.assert_array_equal(out[0], out[1])  # (NaN rows compare equal)
+    assert np.isnan(out[0][200, K:]).all() and not np.isnan(out[0][200, :K]).any()
+    ok = np.ones(T, bool)
+    ok[200] = False  # (the oracle refuses invalid counts)
+    E_ref = oracle.emission(p, d["meth_control"][ok], d["tot_control"][ok], d["meth_case"][ok], d["tot_case"][ok])
+    np.testing.assert_array_equal(out[0][ok], E_ref)
+    assert np.all(out[0][100:130] == 0.0)
