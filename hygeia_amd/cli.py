@@ -159,9 +159,7 @@ def chain_id(chrom: str, batch: int) -> int:
 def _gz_prefix(path: str, max_rows: int):
     """(the bytes of the first max_rows lines of a (multi-member) gzip file,
     whether the file goes on past them). Decompression is most of a parse."""
-    import zlib
-
-    out, lines, more = [], 0, False
+    out, lines = [], 0
     with open(path, "rb") as fh:
         d = zlib.decompressobj(wbits=47)  # gzip or zlib header, auto-detected
         while True:
@@ -183,7 +181,7 @@ def _gz_prefix(path: str, max_rows: int):
                 if c:
                     d = zlib.decompressobj(wbits=47)
         out.append(d.flush())
-    return b"".join(out), more
+    return b"".join(out), False
 
 
 def _read_matrix(path: str, max_rows: int = None) -> np.ndarray:

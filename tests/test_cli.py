@@ -405,3 +405,17 @@ def test_parse_cache(tmp_path):
     task.mkdir(parents=True)
     (task / ".command.sh").write_text("hygeia infer\n")
     assert cli.parse_cache_dir({}, cwd=str(task)) == str(tmp_path / "work" / ".hygeia_parse_cache")
+
+
+def test_partial_read_of_a_multi_member_gzip(tmp_path):
+    """A gzip file of several members (concatenated gzip streams, as `cat a.gz
+    b.gz` makes) reads the same whole and by prefix, across the member joins."""
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, 300, (9_000, 2)).astype(np.float64)
+    p = tmp_path / "m.txt.gz"
+    with open(p, "wb") as fh:
+        for part in (a[:4000], a[4000:4001], a[4001:]):
+            fh.write(gzip.compress(("\n".join(",".join(str(int(v)) for v in r) for r in part) + "\n").encode()))
+    np.testing.assert_array_equal(cli._read_matrix(str(p)), a)
+    for n in (3999, 4000, 4001, 4002, 8999, 9000, 20_000):
+        np.testing.assert_array_equal(cli._read_matrix(str(p), max_rows=n), a[:n])
