@@ -28,11 +28,17 @@ import math
 import os
 import re
 import sys
+import threading
 import time
 import zlib
 from typing import Dict, List, Sequence
 
 import numpy as np
+
+try:  # on the importing (main) thread, before any reader thread: see _import_parsers
+    import pyarrow  # noqa: F401
+except ImportError:  # pragma: no cover -- the readers then fall back to pandas
+    pass
 
 # (name, kind, default, help) in the reference's definition order (:19-72)
 FLAGS_SPEC = [
@@ -184,6 +190,27 @@ def _gz_prefix(path: str, max_rows: int):
     return b"".join(out), False
 
 
+_IMPORT_LOCK = threading.Lock()
+
+
+def _import_parsers(pandas: bool = False):
+    """pyarrow.csv (or pandas) for the readers, which run on worker threads
+    (_read_inputs), imported under one process-wide lock. pyarrow itself must
+    already have been imported by the main thread (this module's import does
+    it): with pyarrow 25 / numpy 2.2 a process whose first `import pyarrow`
+    ran on a worker thread segfaults inside ChunkedArray.to_numpy when several
+    threads convert at once (tests/test_cli.py::
+    test_parallel_reads_after_module_import)."""
+    with _IMPORT_LOCK:
+        if pandas:
+            import pandas as pd
+
+            return pd
+        import pyarrow.csv as pacsv
+
+        return pacsv
+
+
 def _read_matrix(path: str, max_rows: int = None) -> np.ndarray:
     """A whole-chromosome count matrix (run_inference_two_groups.py:177-191 reads
     it with pd.read_table(sep=",", header=None)) as float64; with max_rows, only
@@ -199,8 +226,7 @@ def _read_matrix(path: str, max_rows: int = None) -> np.ndarray:
     import io
 
     try:
-        import pyarrow.csv as pacsv
-
+        pacsv = _import_parsers()
         ro = pacsv.ReadOptions(autogenerate_column_names=True)
         po = pacsv.ParseOptions(delimiter=",")
         if max_rows is None or not path.endswith(".gz"):
@@ -219,8 +245,7 @@ def _read_matrix(path: str, max_rows: int = None) -> np.ndarray:
                 return a
     except Exception:  # noqa: BLE001 -- any pyarrow failure (ArrowInvalid, ArrowNotImplementedError,
         pass  # ArrowTypeError, ...) falls back to pandas, the reference's parser
-    import pandas as pd
-
+    pd = _import_parsers(pandas=True)
     return pd.read_csv(path, sep=",", header=None, dtype=np.float64, nrows=max_rows).to_numpy()
 
 
@@ -359,6 +384,18 @@ def pandas_float(s: str) -> float:
     return number / _POW10F[-exponent]
 
 
+def control_theta(theta: np.ndarray, K: int, chrom: str = "") -> np.ndarray:
+    """get_estimated_control_group_param (run_inference_two_groups.py:76-89):
+    P's rows from the first K (K - 1) entries, omega's logits from the LAST K.
+    A theta of the single-group step with kappa estimated (K (K + 1) entries,
+    model_functions.R:65-78) therefore gives log kappa as omega's logits, as
+    the reference reads it. Other lengths are refused."""
+    n = theta.shape[0]
+    if n not in (K * K, K * (K + 1)):
+        raise ValueError(f"theta_{chrom}.csv.gz holds {n} values, expected K^2 = {K * K} (or K(K+1) = {K * (K + 1)})")
+    return np.concatenate([theta[:K * (K - 1)], theta[n - K:]])
+
+
 def read_theta(single_group_dir: str, chrom: str) -> np.ndarray:
     """theta_{chrom}.csv.gz, column 'data' (run_inference_two_groups.py:76-79),
     with pandas' values, the reference's reader: pandas' default float
@@ -483,9 +520,7 @@ def infer(argv: Sequence[str]) -> int:
     mu = np.array([float(x) for x in f["mu"]], dtype=np.float32)
     sigma = np.array([float(x) for x in f["sigma"]], dtype=np.float32)
     K = mu.shape[0]
-    theta = read_theta(str(f["single_group_dir"]), chrom)
-    if theta.shape[0] != K * K:
-        raise ValueError(f"theta_{chrom}.csv.gz holds {theta.shape[0]} values, expected K^2 = {K * K}")
+    theta = control_theta(read_theta(str(f["single_group_dir"]), chrom), K, chrom)
 
     LAST_TIMINGS.clear()
     t_parse = time.perf_counter()
@@ -683,9 +718,7 @@ def infer_many(argv: Sequence[str]) -> int:
     mu = np.array([float(x) for x in f["mu"]], dtype=np.float32)
     sigma = np.array([float(x) for x in f["sigma"]], dtype=np.float32)
     K = mu.shape[0]
-    theta = read_theta(str(f["single_group_dir"]), chrom)
-    if theta.shape[0] != K * K:
-        raise ValueError(f"theta_{chrom}.csv.gz holds {theta.shape[0]} values, expected K^2 = {K * K}")
+    theta = control_theta(read_theta(str(f["single_group_dir"]), chrom), K, chrom)
     LAST_TIMINGS.clear()
     t_parse = time.perf_counter()
     positions, tot_c, meth_c, tot_k, meth_k = _read_inputs(str(f["data_dir"]), chrom)

@@ -419,3 +419,40 @@ def test_partial_read_of_a_multi_member_gzip(tmp_path):
     np.testing.assert_array_equal(cli._read_matrix(str(p)), a)
     for n in (3999, 4000, 4001, 4002, 8999, 9000, 20_000):
         np.testing.assert_array_equal(cli._read_matrix(str(p), max_rows=n), a[:n])
+
+
+def test_control_theta_slices_as_the_reference():
+    """get_estimated_control_group_param (run_inference_two_groups.py:76-89):
+    P from the first K (K - 1) entries, omega's logits from the last K -- for a
+    K (K + 1) theta (kappa estimated) those are the log kappa entries."""
+    K = 6
+    th = np.arange(42, dtype=np.float64)
+    np.testing.assert_array_equal(cli.control_theta(th[:36], K), th[:36])
+    np.testing.assert_array_equal(cli.control_theta(th, K), np.concatenate([th[:30], th[36:]]))
+    with pytest.raises(ValueError):
+        cli.control_theta(th[:40], K)
+
+
+def test_parallel_reads_after_module_import(tmp_path):
+    """_read_inputs parses its five files on worker threads. With pyarrow 25 /
+    numpy 2.2 a process whose first `import pyarrow` happened on a worker
+    thread segfaults in ChunkedArray.to_numpy under concurrent conversions;
+    importing hygeia_amd.cli imports pyarrow on the main thread first. A fresh
+    interpreter runs many concurrent reads and must exit cleanly."""
+    import subprocess
+    import sys
+
+    rng = np.random.default_rng(5)
+    p = str(tmp_path / "a.txt.gz")
+    np.savetxt(p, rng.integers(0, 500, (20_000, 3)).astype(np.float64), fmt="%.18e", delimiter=",")
+    code = (
+        "import sys\n"
+        "from concurrent.futures import ThreadPoolExecutor\n"
+        "from hygeia_amd import cli\n"
+        "for _ in range(20):\n"
+        "    with ThreadPoolExecutor(8) as ex:\n"
+        "        list(ex.map(lambda n: cli._read_matrix(sys.argv[1], n), [None, 5, 19999, 20000, 10 ** 6] * 4))\n"
+    )
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code, p], cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
