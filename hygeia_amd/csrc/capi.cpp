@@ -816,12 +816,11 @@ int hyg_sg_run_chains_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, cons
   if (psi_capacity < 0 || psi_capacity > (1 << 24)) return fail(HYG_EINVAL, "psi_capacity out of range");
   hyg_sgpe_consts pc{};
   int rc = hyg_sgpe_consts_make(&m->params, pe, &pc);
-  if (rc == HYG_EUNSUPPORTED) return fail(rc, "parameter estimation needs is_kappa_fixed (the pipeline default)");
   if (rc != HYG_OK) return fail(rc, "invalid parameter-estimation settings");
   const int cap = psi_capacity ? psi_capacity : kSgPsiCapDefault;
   if (workspace_bytes < hyg_sg_pe_workspace_bytes(m, chains, n_chains, psi_capacity))
     return fail(HYG_EINVAL, "workspace too small (see hyg_sg_pe_workspace_bytes)");
-  const int K = m->c.K, dim = K * K;
+  const int K = m->c.K, dim = pc.dim;  // theta length: K^2, or K (K + 1) with kappa estimated
   std::vector<SgChainDev> cd(n_chains);
   size_t off = sg_header_bytes(n_chains);
   const size_t per = sg_chain_ws_bytes(K, cap);
@@ -849,17 +848,19 @@ int hyg_sg_run_chains_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, cons
     off += per;
     pe_off += sg_pe_region_bytes(K, cd[i].rcap);
   }
-  // model-level inputs: theta0 [dim] | steps [max_rows] | lgk [K][max_rcap]
+  // model-level inputs: theta0 [dim] | steps [max_rows] | lgk [K][max_rcap] | dgk [K][max_rcap] (kappa estimated)
   std::vector<hyg_sgpe_step> steps((size_t)max_rows);
   hyg_sgpe_steps_fill(pe, (int)max_rows, steps.data());
-  std::vector<double> lgk((size_t)K * max_rcap);
+  std::vector<double> lgk((size_t)K * max_rcap), dgk(pc.kest ? (size_t)K * max_rcap : 0);
   hyg_sgpe_lgk_fill(pc.kappa, K, max_rcap, lgk.data());
+  if (pc.kest) hyg_sgpe_dgk_fill(pc.kappa, K, max_rcap, dgk.data());
   const size_t b_th = sizeof(double) * dim, b_st = sizeof(hyg_sgpe_step) * steps.size(),
-               b_lg = sizeof(double) * lgk.size();
-  std::vector<unsigned char> host(b_th + b_st + b_lg);
+               b_lg = sizeof(double) * lgk.size(), b_dg = sizeof(double) * dgk.size();
+  std::vector<unsigned char> host(b_th + b_st + b_lg + b_dg);
   std::memcpy(host.data(), m->params.theta, b_th);
   std::memcpy(host.data() + b_th, steps.data(), b_st);
   std::memcpy(host.data() + b_th + b_st, lgk.data(), b_lg);
+  if (b_dg) std::memcpy(host.data() + b_th + b_st + b_lg, dgk.data(), b_dg);
   hipStream_t s = (hipStream_t)stream;
   void* dbuf = nullptr;
   if (hipMallocAsync(&dbuf, host.size(), s) != hipSuccess) return fail(HYG_ENOMEM, "device allocation failed");
@@ -878,6 +879,7 @@ int hyg_sg_run_chains_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, cons
   pd.theta0 = (const double*)dbuf;
   pd.steps = (const hyg_sgpe_step*)((unsigned char*)dbuf + b_th);
   pd.lgk = (const double*)((unsigned char*)dbuf + b_th + b_st);
+  pd.dgk = pc.kest ? (const double*)((unsigned char*)dbuf + b_th + b_st + b_lg) : nullptr;
   pd.lgk_stride = max_rcap;
   pd.theta_out = theta_out;
   int32_t* st = status ? status : (int32_t*)(ws + sizeof(SgChainDev) * n_chains);
@@ -914,7 +916,8 @@ int hyg_sg_run_chain_host_pe(const hyg_sg_model* m, const hyg_sg_pe_params* pe, 
   const size_t nc = (size_t)T * S;
   const size_t wsb = hyg_sg_pe_workspace_bytes(m, &ch, 1, 0);
   const int64_t rows = hyg_sgpe_theta_rows(T, pe->n_steps_without_update);
-  const size_t thb = sizeof(double) * (size_t)rows * K * K;
+  const int dth = m->params.is_kappa_fixed ? K * K : K * (K + 1);
+  const size_t thb = sizeof(double) * (size_t)rows * dth;
   bool ok = alloc(b_m, nc * 2) && alloc(b_t, nc * 2) && alloc(b_E, sizeof(double) * T * K) && alloc(b_ws, wsb) &&
             alloc(b_p, sizeof(double) * T * K) && alloc(b_st, 4) && alloc(b_th, thb);
   if (!ok) return fail(HYG_ENOMEM, "device allocation failed");

@@ -48,17 +48,20 @@ struct SgPeDev {
   const double* theta0;        // [dim] initial theta
   const hyg_sgpe_step* steps;  // [n] step sizes / bias corrections per update
   const double* lgk;           // [K][lgk_stride] theta-free part of the NegBin log-pmf
+  const double* dgk;           // [K][lgk_stride] psi(x + kappa) - psi(kappa) (kappa estimated), else null
   int32_t lgk_stride;
   int32_t pad;
-  double* theta_out;           // [rows][dim]
+  double* theta_out;           // [rows][c.dim]
 };
 
-// Per-chain region of the estimation path: phi [2][256][dim], theta, ADAM
-// moments, previous / current score [dim] each, hazard rows [K][rcap], and
-// the rebuild scratch h, g, bigH[d-1], gradBigH[d-1] [K][rcap] f64 + exit [K][rcap] u8.
+// Per-chain region of the estimation path: phi [2][256][K^2] (the kappa
+// coordinates' score is identically 0, include/hyg_sg_pe.h), theta, ADAM
+// moments, previous / current score [K (K + 1)] each, hazard rows [K][rcap],
+// and the rebuild scratch h, g, gk, bigH[d-1], gradBigH[d-1] [K][rcap] f64 +
+// exit [K][rcap] u8.
 __host__ __device__ inline size_t sg_pe_region_bytes(int K, int rcap) {
-  const size_t dim = (size_t)K * K;
-  const size_t b = 8 * (2 * (size_t)kSgThreads * dim + 5 * dim) + 32 * (size_t)K * rcap + 32 * (size_t)K * rcap +
+  const size_t dim = (size_t)K * K, dth = (size_t)K * (K + 1);
+  const size_t b = 8 * (2 * (size_t)kSgThreads * dim + 5 * dth) + 32 * (size_t)K * rcap + 40 * (size_t)K * rcap +
                    (size_t)K * rcap;
   return (b + 255) / 256 * 256;
 }

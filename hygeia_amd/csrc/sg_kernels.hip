@@ -315,26 +315,27 @@ sg_emission_kernel(const double* __restrict__ lf, const double* __restrict__ lg,
 // ------------------------------------------- parameter estimation helpers
 // The chain's region of the workspace (sg_pe_region_bytes).
 struct SgPeChain {
-  double* phi;  // [2][NT][dim] score recursion, particle-major
-  double *th, *am, *av, *gp, *gc;
+  double* phi;  // [2][NT][K^2] score recursion, particle-major
+  double *th, *am, *av, *gp, *gc;  // [K (K + 1)] (theta rows are c.dim wide)
   hyg_sgpe_row* rows;            // [K][rcap]
-  double *h, *g, *Hm1, *gm1;     // rebuild scratch [K][rcap]
+  double *h, *g, *gk, *Hm1, *gm1; // rebuild scratch [K][rcap]
   uint8_t* ex;                   // [K][rcap]
   int rcap;
 };
 __device__ __forceinline__ SgPeChain sg_pe_chain(uint8_t* ws, const SgChainDev& ch, int K) {
   SgPeChain c;
-  const size_t dim = (size_t)K * K, kr = (size_t)K * ch.rcap;
+  const size_t dim = (size_t)K * K, dth = (size_t)K * (K + 1), kr = (size_t)K * ch.rcap;
   c.phi = (double*)(ws + ch.pe_offset);
   c.th = c.phi + 2 * (size_t)kSgThreads * dim;
-  c.am = c.th + dim;
-  c.av = c.am + dim;
-  c.gp = c.av + dim;
-  c.gc = c.gp + dim;
-  c.rows = (hyg_sgpe_row*)(c.gc + dim);
+  c.am = c.th + dth;
+  c.av = c.am + dth;
+  c.gp = c.av + dth;
+  c.gc = c.gp + dth;
+  c.rows = (hyg_sgpe_row*)(c.gc + dth);
   c.h = (double*)(c.rows + kr);
   c.g = c.h + kr;
-  c.Hm1 = c.g + kr;
+  c.gk = c.g + kr;
+  c.Hm1 = c.gk + kr;
   c.gm1 = c.Hm1 + kr;
   c.ex = (uint8_t*)(c.gm1 + kr);
   c.rcap = ch.rcap;
@@ -353,27 +354,32 @@ __device__ void sg_pe_rebuild(const SgPeDev& pe, const hyg_sg_consts& c, const S
   if (L > pc.rcap) L = pc.rcap;
   if (tid < K) hyg_sgpe_set_regime(pc.th, K, tid, pm);
   __syncthreads();
+  const bool kest = pe.dgk != nullptr;  // kappa estimated: the omega coordinate takes d log rho / d theta_kappa
   for (int i = tid; i < K * L; i += NB) {
     const int r = i / L, d = i - r * L;
-    double h, g;
-    hyg_sgpe_hazard_point(pm, r, d, u, c.kappa[r], pe.lgk + (size_t)r * pe.lgk_stride, &h, &g);
+    double h, g, gk;
+    hyg_sgpe_hazard_point(pm, r, d, u, c.kappa[r], pe.lgk + (size_t)r * pe.lgk_stride,
+                          kest ? pe.dgk + (size_t)r * pe.lgk_stride : nullptr, &h, &g, &gk);
     const size_t o = (size_t)r * pc.rcap + d;
     pc.h[o] = h;
     pc.g[o] = g;
+    if (kest) pc.gk[o] = gk;
   }
   __syncthreads();
   if (tid < K) {
     const size_t o = (size_t)tid * pc.rcap;
-    const int l = hyg_sgpe_hazard_scan(pc.h + o, pc.g + o, u, L, pc.Hm1 + o, pc.gm1 + o, pc.ex + o);
+    const int l =
+        hyg_sgpe_hazard_scan(pc.h + o, pc.g + o, kest ? pc.gk + o : nullptr, u, L, pc.Hm1 + o, pc.gm1 + o, pc.ex + o);
     Lr[tid] = l;
     exr[tid] = pc.ex[o + l - 1];
   }
   __syncthreads();
+  const double* gsel = kest ? pc.gk : pc.g;
   for (int i = tid; i < K * L; i += NB) {
     const int r = i / L, d = i - r * L;
     if (d < Lr[r]) {
       const size_t o = (size_t)r * pc.rcap + d;
-      pc.rows[o] = hyg_sgpe_hazard_row(pc.h[o], pc.g[o], pc.Hm1[o], pc.gm1[o], pc.ex[o], d, u);
+      pc.rows[o] = hyg_sgpe_hazard_row(pc.h[o], gsel[o], pc.Hm1[o], pc.gm1[o], pc.ex[o], d, u);
     }
   }
   __syncthreads();
@@ -614,17 +620,20 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
   int* peEx = PE ? peLr + HYG_KMAX : nullptr;              // [KMAX] exited at the last row
   int8_t* rpu = PE ? (int8_t*)(smem + lay.rpu) : nullptr;  // [2][NT] r if d >= u else -1
   SgPeChain pc{};
+  // phi holds the K^2 P / omega coordinates; with kappa estimated theta has
+  // K more (dth = K (K + 1)) whose score is identically 0 (include/hyg_sg_pe.h)
   constexpr int dim = K * K, jw = K * (K - 1);
   const int every = PE ? pe.c.every : 1;
+  const int dth = PE ? pe.c.dim : dim;
   if constexpr (PE) {
     pc = sg_pe_chain(ws, ch, K);
-    for (int j = tid; j < dim; j += NB) {
+    for (int j = tid; j < dth; j += NB) {
       const double th0 = pe.theta0[j];
       pc.th[j] = th0;
       pc.am[j] = 0.0;
       pc.av[j] = 0.0;
       pc.gp[j] = 0.0;  // gradientCurr at t = 0: the filtered mean of phi = 0
-      pe.theta_out[(size_t)ch.theta_row * dim + j] = th0;
+      pe.theta_out[(size_t)ch.theta_row * dth + j] = th0;
     }
     for (int i = tid; i < K * dim; i += NB) pc.phi[i] = 0.0;  // phi of the K initial particles
     __syncthreads();
@@ -1339,15 +1348,17 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
           // updateGradients (:151-156): filtered mean of phi, difference to the
           // previous one; GradientAscent::iterate (GradientAscent.h:82-105)
           const double* wCur = w_ + cb * NT;
-          for (int j = tid; j < dim; j += NB) {
-            double est = 0.0;
-            for (int n0 = 0; n0 < N; n0 += kFb) {
-              double v[kFb];
+          for (int j = tid; j < dth; j += NB) {
+            double est = 0.0;  // the kappa coordinates (j >= K^2): sum_n W_n (+0) = +0
+            if (j < dim) {
+              for (int n0 = 0; n0 < N; n0 += kFb) {
+                double v[kFb];
 #pragma unroll
-              for (int i = 0; i < kFb; ++i) v[i] = phiC[(size_t)(n0 + i) * dim + j];
+                for (int i = 0; i < kFb; ++i) v[i] = phiC[(size_t)(n0 + i) * dim + j];
 #pragma unroll
-              for (int i = 0; i < kFb; ++i)
-                if (n0 + i < N) est = est + wCur[n0 + i] * v[i];
+                for (int i = 0; i < kFb; ++i)
+                  if (n0 + i < N) est = est + wCur[n0 + i] * v[i];
+              }
             }
             pc.gc[j] = est - pc.gp[j];
             pc.gp[j] = est;
@@ -1355,17 +1366,17 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
           __syncthreads();
           double l1 = 0.0;
           if (pe.c.normalise && !pe.c.use_adam)
-            for (int j = 0; j < dim; ++j) l1 = l1 + fabs(pc.gc[j]);
+            for (int j = 0; j < dth; ++j) l1 = l1 + fabs(pc.gc[j]);
           const int it = t / every - 1;
           const double lr = pe.steps[it].lr, c1 = pe.steps[it].c1, c2 = pe.steps[it].c2;
-          for (int j = tid; j < dim; j += NB) {
+          for (int j = tid; j < dth; j += NB) {
             double am = pc.am[j], av = pc.av[j];
             const double th = hyg_sgpe_update(pe.c.use_adam, pe.c.normalise, pe.c.beta1, pe.c.beta2, pe.c.eps, lr,
                                               c1, c2, pc.th[j], pc.gc[j], l1, &am, &av);
             pc.th[j] = th;
             pc.am[j] = am;
             pc.av[j] = av;
-            pe.theta_out[(size_t)(ch.theta_row + t / every) * dim + j] = th;
+            pe.theta_out[(size_t)(ch.theta_row + t / every) * dth + j] = th;
           }
           // rows for every sojourn the set can reach before the next rebuild
           const int maxd = (int)block_max<NB>((tid < N) ? (double)sg_d(my_st) : 0.0, red);

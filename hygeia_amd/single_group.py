@@ -167,22 +167,27 @@ def default_p(K: int) -> np.ndarray:
     return v.reshape(K, K, order="F")
 
 
-def theta_from_model(p: np.ndarray, omega: np.ndarray) -> np.ndarray:
-    """convert_model_parameters_to_theta (model_functions.R:62-76), kappa fixed:
+def theta_from_model(p: np.ndarray, omega: np.ndarray, kappa=None) -> np.ndarray:
+    """convert_model_parameters_to_theta (model_functions.R:65-78):
     diag(p) <- -1; c(log(p[p != -1]), logit(omega)) -- p[p != -1] in R's
-    column-major order."""
+    column-major order -- and log(kappa) appended when kappa is estimated
+    (kappa given)."""
     p = np.array(p, dtype=np.float64)
     np.fill_diagonal(p, -1.0)
     flat = p.flatten(order="F")
     off = flat[flat != -1.0]
     with np.errstate(divide="ignore"):
-        return np.concatenate([np.log(off), np.log(omega) - np.log(1.0 - omega)])
+        parts = [np.log(off), np.log(omega) - np.log(1.0 - omega)]
+        if kappa is not None:
+            parts.append(np.log(np.asarray(kappa, dtype=np.float64)))
+        return np.concatenate(parts)
 
 
 def model_from_theta(theta: np.ndarray, K: int):
-    """convert_theta_to_model_parameters (model_functions.R:78-111), kappa fixed:
-    row r of p = exp(normalise_exp(theta block r)) off the diagonal (row-major),
-    omega = inverse_logit(theta[K(K-1):K^2])."""
+    """convert_theta_to_model_parameters (model_functions.R:81-111): row r of p
+    = exp(normalise_exp(theta block r)) off the diagonal (row-major), omega =
+    inverse_logit(theta[K(K-1):K^2]) and, when theta carries the K log kappa
+    entries (kappa estimated), kappa = exp(theta[K^2:K(K+1)]) (else None)."""
     p = np.zeros((K, K))
     for r in range(K):
         blk = theta[r * (K - 1):(r + 1) * (K - 1)]
@@ -190,7 +195,8 @@ def model_from_theta(theta: np.ndarray, K: int):
         lz = m + math.log(np.exp(blk - m).sum())
         p[r, [c for c in range(K) if c != r]] = np.exp(blk - lz)
     omega = 1.0 / (1.0 + np.exp(-theta[K * (K - 1):K * K]))
-    return p, omega
+    kappa = np.exp(theta[K * K:K * (K + 1)]) if theta.shape[0] >= K * (K + 1) else None
+    return p, omega, kappa
 
 
 # ------------------------------------------------------------------ outputs
@@ -279,20 +285,27 @@ def write_regimes(path: str, positions: np.ndarray, probs: np.ndarray) -> None:
 
 # ------------------------------------------------------------------- engine
 def run_engine(L, K: int, u: int, alpha, beta, kappa, theta_init, epsilon: float, n_particles: int,
-               meth: np.ndarray, tot: np.ndarray, seed: int, chain_id: int, estimate_parameters: bool, pe_flags=None):
+               meth: np.ndarray, tot: np.ndarray, seed: int, chain_id: int, estimate_parameters: bool, pe_flags=None,
+               is_kappa_fixed: bool = True):
     """runOnlineCombinedInferenceCpp (singleGroup.cpp:76-189) through the C ABI:
     regime probabilities [T][K] and, with parameter estimation, the engine's
-    theta rows [1 + (T - 1) / every][K^2]."""
+    theta rows [1 + (T - 1) / every][dim] (dim = K^2, or K (K + 1) with kappa
+    estimated: then theta_init carries log kappa and `kappa` is unused, as
+    vartheta has no kappa, model_functions.R:48-54)."""
     import ctypes as C
 
     from . import _lib
 
+    dim = K * K if is_kappa_fixed else K * (K + 1)
+    if len(theta_init) != dim:
+        raise ValueError(f"theta has {len(theta_init)} entries, the model {dim}")
     p = _lib.SgParams()
     L.hyg_sg_params_default(C.byref(p))
     p.n_regimes, p.minimum_duration, p.num_particles_max = K, int(u), int(n_particles)
-    p.resample_type, p.is_kappa_fixed, p.theta_len = 2, 1, K * K
+    p.resample_type, p.is_kappa_fixed, p.theta_len = 2, int(bool(is_kappa_fixed)), dim
     for r in range(K):
-        p.alpha[r], p.beta[r], p.kappa[r] = float(alpha[r]), float(beta[r]), float(kappa[r])
+        p.alpha[r], p.beta[r] = float(alpha[r]), float(beta[r])
+        p.kappa[r] = float(kappa[r]) if is_kappa_fixed else 0.0
     for i, v in enumerate(theta_init):
         p.theta[i] = float(v)
     p.epsilon = float(epsilon)
@@ -316,7 +329,7 @@ def run_engine(L, K: int, u: int, alpha, beta, kappa, theta_init, epsilon: float
         pe.learning_rate_factor = float(pe_flags["learning_rate_factor"])
         ch = _lib.SgChain(0, T, 0, seed, chain_id, 0)
         rows = int(L.hyg_sg_pe_theta_rows(C.byref(ch), 1, pe.n_steps_without_update))
-        theta = np.empty((rows, K * K), np.float64)
+        theta = np.empty((rows, dim), np.float64)
         _lib.check(L.hyg_sg_run_chain_host_pe(h, C.byref(pe), ptr(meth), ptr(tot), S, T, seed, chain_id, ptr(probs),
                                               ptr(theta)))
         return probs, theta
@@ -337,9 +350,8 @@ def main(argv: Sequence[str]) -> int:
     sigma, mu = _numbers(f["sigma"]), _numbers(f["mu"])
     K = mu.shape[0]
     p = read_csv_matrix(f["p_input_csv_file"]) if f["p_input_csv_file"] else default_p(K)
-    if not f["is_kappa_fixed"]:
-        raise NotImplementedError("--is_kappa_fixed FALSE: the estimated-kappa branch writes its gradient into "
-                                  "the omega entries (singleGroup.h:656-661); only fixed kappa is supported")
+    fixed = bool(f["is_kappa_fixed"])
+    dim_theta = K * K if fixed else K * (K + 1)  # get_known_parameters (model_functions.R:48-54)
     for path in (f["n_methylated_reads_csv_file"], f["genomic_positions_csv_file"], f["n_total_reads_csv_file"],
                  f["regime_probabilities_csv_file"], f["theta_trace_csv_file"], f["p_csv_file"],
                  f["omega_csv_file"], f["kappa_csv_file"], f["theta_file"]):  # create_dirs_for_file (:250-262)
@@ -349,9 +361,9 @@ def main(argv: Sequence[str]) -> int:
     nu = mu * (1 - mu) / sigma ** 2 - 1
     alpha, beta = mu * nu, (1 - mu) * nu
     if f["estimate_parameters"]:  # sampleFromParameterPriorCpp: theta ~ N(0, I) (singleGroup.h:480-483)
-        theta_init = np.random.default_rng(seed).standard_normal(K * K)
+        theta_init = np.random.default_rng(seed).standard_normal(dim_theta)
     else:
-        theta_init = theta_from_model(p, omega)
+        theta_init = theta_from_model(p, omega, None if fixed else kappa)
     positions = read_csv_matrix(f["genomic_positions_csv_file"])[:, 0]
     tot = read_csv_matrix(f["n_total_reads_csv_file"])
     meth = read_csv_matrix(f["n_methylated_reads_csv_file"])
@@ -367,7 +379,7 @@ def main(argv: Sequence[str]) -> int:
     L = _lib.load(import_torch=False)
     _use_task_device(L)
     probs, theta = run_engine(L, K, u, alpha, beta, kappa, theta_init, f["epsilon"], f["n_particles"], meth, tot,
-                              seed, 0, bool(f["estimate_parameters"]), f)
+                              seed, 0, bool(f["estimate_parameters"]), f, is_kappa_fixed=fixed)
     if f["estimate_regime_probabilities"]:
         write_regimes(f["regime_probabilities_csv_file"], positions, probs)
     if f["estimate_parameters"]:
@@ -375,11 +387,12 @@ def main(argv: Sequence[str]) -> int:
         every = int(f["n_steps_without_parameter_update"])
         write_theta_trace(f["theta_trace_csv_file"], theta, T, every)
         last = theta[(T - 1) // every]
-        p_hat, omega_hat = model_from_theta(last, K)
+        p_hat, omega_hat, kappa_hat = model_from_theta(last, K)
         write_csv(f["p_csv_file"], [f"regime_{r + 1}" for r in range(K)],
                   [[_shortest(v) for v in p_hat[:, c]] for c in range(K)])
         write_vector(f["omega_csv_file"], "omega", omega_hat)
-        write_vector(f["kappa_csv_file"], "kappa", kappa)
+        # the final estimate when kappa is estimated, else the given kappa (:363-369)
+        write_vector(f["kappa_csv_file"], "kappa", kappa if fixed else kappa_hat)
         write_vector(f["theta_file"], "data", last, exp17=True)
     return 0
 

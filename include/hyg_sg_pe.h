@@ -18,10 +18,28 @@
  * Arithmetic contract: hyg_exp / hyg_log of include/hyg_arith.h, IEEE
  * + - * / sqrt, no FMA contraction; sums in the reference's sequential order.
  * The lgamma part of the NegBin log-pmf does not depend on theta (kappa is
- * fixed, the pipeline default --is_kappa_fixed TRUE) and is tabulated once on
- * the host with libm lgamma (hyg_sgpe_lgk_fill); the ADAM step sizes and bias
- * corrections are libm pow values tabulated once on the host
- * (hyg_sgpe_steps_fill), as the reference computes them.
+ * fixed, the pipeline default --is_kappa_fixed TRUE, or estimated and then
+ * never moved, see below) and is tabulated once on the host with libm lgamma
+ * (hyg_sgpe_lgk_fill); the ADAM step sizes and bias corrections are libm pow
+ * values tabulated once on the host (hyg_sgpe_steps_fill), as the reference
+ * computes them.
+ *
+ * Estimated kappa (--is_kappa_fixed FALSE): theta gains K entries log kappa_r
+ * (singleGroup.h:114-116,218-223, dim K (K + 1)). The reference's gradient
+ * then writes d log rho / d theta_kappa into the OMEGA index
+ * (singleGroup.h:664-668; its kappa index only ever receives
+ * -grad(idxKappa) rho / (1 - rho) with grad(idxKappa) = 0, :688-692), and that
+ * kappa derivative's bigH recursion adds the OMEGA gradient of bigH
+ * (:329). Restated as written: the omega coordinate carries
+ *   gK(d) = kappa (psi(x + kappa) - psi(kappa) - log(1 - omega))       (:328)
+ *         + gKbigH(d - 1) / (1 - bigH(d - 1)),
+ *   gKbigH(d) = gObigH(d - 1) + h(d) gK_h(d)                            (:329-330)
+ * (x = d + 1 - u), and the kappa coordinates' score is exactly 0 at every
+ * step, so ADAM / gradient ascent leave log kappa where it started (theta +
+ * 0) and kappa = exp(theta_kappa) of the initial theta throughout. The digamma
+ * differences psi(x + kappa) - psi(kappa) are theta-free and tabulated once
+ * on the host (hyg_sgpe_dgk_fill, hyg_digamma below; the reference calls R's
+ * digamma: parity at the last bits unpinned, tests check scipy to 1e-14).
  *
  * Hazard table semantics: rows d = d_prev - 1 = 0 .. L_r - 1 per regime, where
  * L_r = the exit onset + 1 (the first d with exitStatus) or the computed
@@ -80,13 +98,16 @@ HYG_HD void hyg_sgpe_set_regime(const double* theta, int K, int r, hyg_sgpe_mode
 
 /* Hazard row inputs at d (parallel over d): h = NegBin pmf of x = d + 1 - u
  * (misc.h:673-693 evaluateLogNegativeBinomialDensity, lgk = lgamma(x + kappa)
- * - lgamma(kappa) - lgamma(x + 1)) and g = d log h / d theta_omega
- * (singleGroup.h:318). Rows d < u - 1 are 0. */
+ * - lgamma(kappa) - lgamma(x + 1)), g = d log h / d theta_omega
+ * (singleGroup.h:322) and, when kappa is estimated (dgk != NULL: dgk[x] =
+ * psi(x + kappa) - psi(kappa)), gk = d log h / d theta_kappa (:328). Rows
+ * d < u - 1 are 0. */
 HYG_HD void hyg_sgpe_hazard_point(const hyg_sgpe_model* m, int r, int d, int u, double kappa, const double* lgk,
-                                  double* h, double* g) {
+                                  const double* dgk, double* h, double* g, double* gk) {
   if (d < u - 1) {
     *h = 0.0;
     *g = 0.0;
+    if (dgk) *gk = 0.0;
     return;
   }
   const int x = d + 1 - u;
@@ -96,23 +117,27 @@ HYG_HD void hyg_sgpe_hazard_point(const hyg_sgpe_model* m, int r, int d, int u, 
   else lnb = (lgk[x] + kappa * m->log1mw[r]) + (double)x * m->logw[r];
   *h = hyg_exp(lnb);
   *g = ((double)x / w - kappa / (1.0 - w)) * m->gl[r];
+  if (dgk) *gk = kappa * (dgk[x] - m->log1mw[r]);
 }
 
 /* Sequential part of extendAuxiliaryQuantities (singleGroup.h:298-331) for one
  * regime over rows 0 .. L-1: records per row the bigH[d-1] and gradBigH[d-1]
  * its rho and d log rho use, and the exit status. Stops at the exit onset.
- * Returns L_r (rows valid). */
-HYG_HD int hyg_sgpe_hazard_scan(const double* h, const double* g, int u, int L, double* Hm1s, double* gm1s,
-                                uint8_t* ex) {
-  double Hm1 = 0.0, gm1 = 0.0;
+ * With gk (kappa estimated) the recorded gradBigH[d-1] is the kappa one,
+ * gradThetaKappaBigH[d] = gradThetaOmegaBigH[d-1] + h[d] gk[d] (:329), the
+ * omega one still accumulated beside it. Returns L_r (rows valid). */
+HYG_HD int hyg_sgpe_hazard_scan(const double* h, const double* g, const double* gk, int u, int L, double* Hm1s,
+                                double* gm1s, uint8_t* ex) {
+  double Hm1 = 0.0, gm1 = 0.0, gkm1 = 0.0;
   /* the inputs are read 16 rows ahead of the sequential recursion (on the GPU
    * one lane per regime runs it: the loads then overlap) */
   for (int d0 = 0; d0 < L; d0 += 16) {
-    double hb[16], gb[16];
+    double hb[16], gb[16], kb[16];
     for (int i = 0; i < 16; ++i) {
       const int d = d0 + i;
       hb[i] = (d < L) ? h[d] : 0.0;
       gb[i] = (d < L) ? g[d] : 0.0;
+      kb[i] = (gk && d < L) ? gk[d] : 0.0;
     }
     for (int i = 0; i < 16; ++i) {
       const int d = d0 + i;
@@ -125,13 +150,14 @@ HYG_HD int hyg_sgpe_hazard_scan(const double* h, const double* g, int u, int L, 
       }
       if (Hm1 >= 1.0) { /* exit onset: bigH[d-1] is overwritten with 0.99999 */
         Hm1s[d] = HYG_SGPE_EXIT_H;
-        gm1s[d] = gm1;
+        gm1s[d] = gk ? gkm1 : gm1;
         ex[d] = 1;
         return d + 1;
       }
       Hm1s[d] = Hm1;
-      gm1s[d] = gm1;
+      gm1s[d] = gk ? gkm1 : gm1;
       ex[d] = 0;
+      gkm1 = gm1 + hb[i] * kb[i];
       Hm1 = Hm1 + hb[i];
       gm1 = gm1 + hb[i] * gb[i];
     }
@@ -139,10 +165,11 @@ HYG_HD int hyg_sgpe_hazard_scan(const double* h, const double* g, int u, int L, 
   return L;
 }
 
-/* One finished hazard row (parallel over d):
+/* One finished hazard row (parallel over d), g / gm1 the omega (kappa fixed)
+ * or the kappa (kappa estimated) derivative inputs:
  *   base  = log rho (the change-point density before log P), 0 after the exit
  *   cont  = log(1 - rho) if !exit && rho <= 1, else -inf   (singleGroup.h:569-608)
- *   gomg  = d log rho / d theta_omega                       (:319)
+ *   gomg  = the omega coordinate's d log rho                (:324 / :330 via :664-668)
  *   gcont = the continuation's gradient entry -gomg rho / (1 - rho) if
  *           !exit && rho < 1, else 0                        (:683-699) */
 typedef struct {
@@ -187,8 +214,9 @@ typedef struct {
 } hyg_sgpe_step;
 
 typedef struct hyg_sgpe_consts {
-  int32_t K, u, dim, every; /* dim = K^2 (kappa fixed), every = nStepsWithoutParameterUpdate */
+  int32_t K, u, dim, every; /* dim = theta length: K^2 (kappa fixed) or K (K + 1); every = nStepsWithoutParameterUpdate */
   int32_t use_adam, normalise;
+  int32_t kest, pad_;       /* kest: kappa estimated (is_kappa_fixed = 0) */
   double beta1, beta2, eps;
   double kappa[HYG_KMAX];
 } hyg_sgpe_consts;
@@ -207,7 +235,7 @@ HYG_HD double hyg_sgpe_update(int use_adam, int normalise, double beta1, double 
     *av = v;
     return theta + ((lr * m) * (1.0 / (sqrt(v / c2) + eps))) / c1;
   }
-  if (normalise) return theta + lr * (grad / l1);
+  if (normalise) return theta + lr * (grad / (l1 != 0.0 ? l1 : 1.0)); /* arma::normalise leaves a zero vector */
   return theta + lr * grad;
 }
 
@@ -226,23 +254,49 @@ static inline void hyg_sgpe_lgk_fill(const double* kappa, int K, int n, double* 
     for (int x = 0; x < n; ++x)
       lgk[(size_t)r * n + x] = (lgamma((double)x + kappa[r]) - lgamma(kappa[r])) - lgamma((double)x + 1.0);
 }
+/* psi(x), x > 0: the recurrence psi(x) = psi(x + 1) - 1/x up to x >= 10, then
+ * the asymptotic series log x - 1/(2x) - sum_k B_2k / (2k x^2k) to k = 8
+ * (truncation < 1e-17 relative at x >= 10). Host only. */
+static inline double hyg_digamma(double x) {
+  if (!(x > 0.0)) return NAN;
+  double acc = 0.0;
+  while (x < 10.0) {
+    acc -= 1.0 / x;
+    x += 1.0;
+  }
+  const double z = 1.0 / (x * x);
+  /* B_2k / (2k): 1/12, -1/120, 1/252, -1/240, 1/132, -691/32760, 1/12, -3617/8160 */
+  const double s = z * (1.0 / 12 - z * (1.0 / 120 - z * (1.0 / 252 - z * (1.0 / 240 - z * (1.0 / 132 -
+                   z * (691.0 / 32760 - z * (1.0 / 12 - z * (3617.0 / 8160))))))));
+  return acc + ((log(x) - 0.5 / x) - s);
+}
+/* dgk[r][x] = psi(x + kappa_r) - psi(kappa_r), x < n (singleGroup.h:328's digamma difference) */
+static inline void hyg_sgpe_dgk_fill(const double* kappa, int K, int n, double* dgk) {
+  for (int r = 0; r < K; ++r) {
+    const double pk = hyg_digamma(kappa[r]);
+    for (int x = 0; x < n; ++x) dgk[(size_t)r * n + x] = hyg_digamma((double)x + kappa[r]) - pk;
+  }
+}
 static inline int hyg_sgpe_consts_make(const hyg_sg_params* p, const hyg_sg_pe_params* pe, hyg_sgpe_consts* c) {
   const int K = p->n_regimes;
-  if (!p->is_kappa_fixed) return HYG_EUNSUPPORTED;
   if (pe->n_steps_without_update < 1) return HYG_EINVAL;
   if (!(pe->learning_rate_factor == pe->learning_rate_factor) ||
       !(pe->learning_rate_exponent == pe->learning_rate_exponent))
     return HYG_EINVAL;
   c->K = K;
   c->u = p->minimum_duration;
-  c->dim = K * K;
+  c->kest = p->is_kappa_fixed ? 0 : 1;
+  c->dim = c->kest ? K * (K + 1) : K * K;
   c->every = pe->n_steps_without_update;
   c->use_adam = pe->use_adam ? 1 : 0;
   c->normalise = pe->normalise_gradients ? 1 : 0;
   c->beta1 = 0.9;
   c->beta2 = 0.999;
   c->eps = exp(-8.0 * log(10.0)); /* GradientAscent.h:60 */
-  for (int r = 0; r < K; ++r) c->kappa[r] = p->kappa[r];
+  /* kappa_r = exp(theta_kappa_r) when estimated (singleGroup.h:218-223), as hyg_sg_derive */
+  for (int r = 0; r < K; ++r) c->kappa[r] = c->kest ? exp(p->theta[K * K + r]) : p->kappa[r];
+  for (int r = 0; r < K; ++r)
+    if (!(c->kappa[r] > 0.0) || !isfinite(c->kappa[r])) return HYG_EINVAL;
   return HYG_OK;
 }
 /* number of theta rows a chain of T sites reports: the initial theta and

@@ -318,7 +318,10 @@ int hyg_sg_run_chain_host(const hyg_sg_model* model, const uint16_t* meth, const
  * --estimate_regime_probabilities --estimate_parameters`
  * (modules/two_group/2_estimate_parameters_and_regimes.nf:38-52). The
  * regime probabilities are smoothed under the moving theta, as the reference.
- * Requires is_kappa_fixed (the pipeline default); else HYG_EUNSUPPORTED. */
+ * With is_kappa_fixed = 0 theta holds K more entries log kappa_r and the
+ * gradient is the reference's as written (singleGroup.h:664-692: the omega
+ * coordinate takes d log rho / d theta_kappa, the kappa coordinates stay put;
+ * include/hyg_sg_pe.h). */
 typedef struct hyg_sg_pe_params {
   int32_t use_adam;               /* --use_adam, TRUE                          */
   int32_t normalise_gradients;    /* --normalise_gradients, FALSE              */
@@ -336,8 +339,8 @@ void hyg_sg_pe_params_default(hyg_sg_pe_params* pe);
 int64_t hyg_sg_pe_theta_rows(const hyg_sg_chain* chains, int32_t n_chains, int32_t every);
 size_t hyg_sg_pe_workspace_bytes(const hyg_sg_model* model, const hyg_sg_chain* chains, int32_t n_chains,
                                  int32_t psi_capacity);
-/* As hyg_sg_run_chains, with theta updated online; theta_out [rows][K^2] f64
- * (device). status may also be HYG_ENOMEM when a sojourn outgrows the
+/* As hyg_sg_run_chains, with theta updated online; theta_out [rows][theta_len]
+ * f64 (device; theta_len = K^2, or K (K + 1) with kappa estimated). status may also be HYG_ENOMEM when a sojourn outgrows the
  * hazard table (HYG_SGPE_DCAP rows) before the hazard's exit. */
 int hyg_sg_run_chains_pe(const hyg_sg_model* model, const hyg_sg_pe_params* pe, const hyg_sg_chain* chains,
                          int32_t n_chains, const double* emission, void* workspace, size_t workspace_bytes,

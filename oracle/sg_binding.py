@@ -78,7 +78,10 @@ def theta_from(P, omega):
     return np.asarray(vals)
 
 
-def make_params(K=6, mu=None, sigma=None, P=None, omega=None, u=3, Nmax=250, epsilon=0.01, kappa=2.0):
+def make_params(K=6, mu=None, sigma=None, P=None, omega=None, u=3, Nmax=250, epsilon=0.01, kappa=2.0,
+                kappa_fixed=True):
+    """hyg_sg_params; kappa_fixed=False: kappa is estimated, theta gains the K
+    entries log kappa (model_functions.R:65-78) and vartheta has no kappa."""
     if mu is None:
         mu = DEFAULT_MU if K == 6 else [(i + 0.5) / K for i in range(K)]
     if sigma is None:
@@ -90,11 +93,14 @@ def make_params(K=6, mu=None, sigma=None, P=None, omega=None, u=3, Nmax=250, eps
         np.fill_diagonal(P, 0.0)
     a, b = beta_params(mu, sigma)
     th = theta_from(P, omega)
+    kap = np.broadcast_to(np.asarray(kappa, float), (K,))
+    if not kappa_fixed:
+        th = np.concatenate([th, np.log(kap)])
     p = SgParams()
     p.n_regimes, p.minimum_duration, p.num_particles_max = K, u, Nmax
-    p.resample_type, p.is_kappa_fixed, p.theta_len = 2, 1, len(th)
+    p.resample_type, p.is_kappa_fixed, p.theta_len = 2, int(bool(kappa_fixed)), len(th)
     for i in range(K):
-        p.alpha[i], p.beta[i], p.kappa[i] = a[i], b[i], kappa
+        p.alpha[i], p.beta[i], p.kappa[i] = a[i], b[i], (kap[i] if kappa_fixed else 0.0)
     for i, v in enumerate(th):
         p.theta[i] = v
     p.epsilon = epsilon
@@ -123,6 +129,8 @@ def lib():
         L.oracle_sg_emission.argtypes = [C.POINTER(SgParams), vp, vp, i32, C.c_int64, vp]
         L.oracle_sg_hazard.restype = i32
         L.oracle_sg_hazard.argtypes = [C.POINTER(SgParams), i32, i32, vp, vp, C.POINTER(i32)]
+        L.oracle_sg_digamma.restype = C.c_double
+        L.oracle_sg_digamma.argtypes = [C.c_double]
         L.oracle_sg_consts.restype = i32
         L.oracle_sg_consts.argtypes = [C.POINTER(SgParams), C.POINTER(SgConsts)]
         assert L.oracle_sizeof_sg_params() == C.sizeof(SgParams)
@@ -194,11 +202,13 @@ def hazard(p, r, n):
 
 def chain_pe(p, pe, E, seed=0, chain_id=0):
     """SMC + online smoothing with online parameter estimation: regime
-    probabilities [T][K] and theta rows [1 + (T-1)//every][K^2]."""
+    probabilities [T][K] and theta rows [1 + (T-1)//every][K^2, or K (K + 1)
+    with kappa estimated]."""
     E = np.ascontiguousarray(E, np.float64)
     T, K = E.shape[0], p.n_regimes
     probs = np.empty((T, K), np.float64)
-    theta = np.full((1 + (T - 1) // pe.n_steps_without_update, K * K), np.nan)
+    dim = K * K if p.is_kappa_fixed else K * (K + 1)
+    theta = np.full((1 + (T - 1) // pe.n_steps_without_update, dim), np.nan)
     rc = lib().oracle_sg_chain_pe(C.byref(p), C.byref(pe), _ptr(E), T, seed, chain_id, _ptr(probs), _ptr(theta))
     return {"status": rc, "regime_probs": probs, "theta": theta}
 
@@ -213,3 +223,8 @@ def pe_hazard(p, theta, L):
     if rc != 0:
         raise ValueError(rc)
     return rows, Lr
+
+
+def digamma(x: float) -> float:
+    """hyg_digamma (include/hyg_sg_pe.h), the psi of the estimated-kappa tables"""
+    return lib().oracle_sg_digamma(float(x))

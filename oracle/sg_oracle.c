@@ -27,7 +27,10 @@
  * order), the filtered score sum_n W_n phi_n (Smc.h:341-350) every
  * `every` steps, the ADAM / gradient step (GradientAscent.h:82-155) and the
  * rebuild of P, omega and the hazard tables from the new theta
- * (include/hyg_sg_pe.h, shared with the kernel).
+ * (include/hyg_sg_pe.h, shared with the kernel). With kappa estimated the
+ * K (K + 1) coordinates are carried literally, the kappa index's gradient
+ * entries as singleGroup.h:664-692 write them (the kernel drops the
+ * identically-zero kappa recursion; the GPU tests compare the two).
  */
 #include <math.h>
 #include <stdint.h>
@@ -54,6 +57,7 @@ typedef struct {
   int overflow;          /* a lookup beyond the rows of a regime that has not exited */
   hyg_sgpe_row* rows;    /* [K][rcap] */
   double *lgk, *h, *g, *Hm1s, *gm1s; /* lgk [K][rcap], scratch [rcap] */
+  double *dgk, *gk;      /* kappa estimated: digamma differences [K][rcap], scratch [rcap] */
   uint8_t* exs;
 } sg_model;
 
@@ -65,12 +69,15 @@ static void sgm_pe_rebuild(sg_model* m, const double* theta, int L) {
   for (int r = 0; r < K; ++r) hyg_sgpe_set_regime(theta, K, r, &m->pm);
   for (int r = 0; r < K; ++r) {
     const double* lgk = m->lgk + (size_t)r * m->rcap;
-    for (int d = 0; d < L; ++d) hyg_sgpe_hazard_point(&m->pm, r, d, u, m->pc.kappa[r], lgk, &m->h[d], &m->g[d]);
-    const int Lr = hyg_sgpe_hazard_scan(m->h, m->g, u, L, m->Hm1s, m->gm1s, m->exs);
+    const double* dgk = m->pc.kest ? m->dgk + (size_t)r * m->rcap : NULL;
+    for (int d = 0; d < L; ++d)
+      hyg_sgpe_hazard_point(&m->pm, r, d, u, m->pc.kappa[r], lgk, dgk, &m->h[d], &m->g[d], &m->gk[d]);
+    const int Lr = hyg_sgpe_hazard_scan(m->h, m->g, dgk ? m->gk : NULL, u, L, m->Hm1s, m->gm1s, m->exs);
     m->Lr[r] = Lr;
     m->exited[r] = m->exs[Lr - 1];
+    const double* gsel = dgk ? m->gk : m->g; /* the omega coordinate's derivative (hyg_sg_pe.h) */
     for (int d = 0; d < Lr; ++d)
-      m->rows[(size_t)r * m->rcap + d] = hyg_sgpe_hazard_row(m->h[d], m->g[d], m->Hm1s[d], m->gm1s[d], m->exs[d], d, u);
+      m->rows[(size_t)r * m->rcap + d] = hyg_sgpe_hazard_row(m->h[d], gsel[d], m->Hm1s[d], m->gm1s[d], m->exs[d], d, u);
   }
 }
 static const hyg_sgpe_row* sgm_pe_row(sg_model* m, int dp, int r) {
@@ -95,7 +102,10 @@ static int sgm_init(sg_model* m, const hyg_sg_params* p, int max_duration) {
 }
 static void sgm_free(sg_model* m) {
   free(m->hz); free(m->ex);
-  if (m->pe) { free(m->rows); free(m->lgk); free(m->h); free(m->g); free(m->Hm1s); free(m->gm1s); free(m->exs); }
+  if (m->pe) {
+    free(m->rows); free(m->lgk); free(m->h); free(m->g); free(m->Hm1s); free(m->gm1s); free(m->exs);
+    free(m->dgk); free(m->gk);
+  }
 }
 
 /* Model::evaluateLogTransitionDensity (singleGroup.h:569-608) for the two
@@ -269,6 +279,8 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
     mo.Hm1s = malloc(sizeof(double) * mo.rcap);
     mo.gm1s = malloc(sizeof(double) * mo.rcap);
     mo.exs = malloc(mo.rcap);
+    mo.gk = malloc(sizeof(double) * mo.rcap);
+    mo.dgk = mo.pc.kest ? malloc(sizeof(double) * (size_t)K * mo.rcap) : NULL;
     theta = malloc(sizeof(double) * dim);
     am = calloc(dim, sizeof(double));
     av = calloc(dim, sizeof(double));
@@ -277,13 +289,14 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
     phiP = calloc((size_t)Nmax * dim, sizeof(double));
     phiC = calloc((size_t)Nmax * dim, sizeof(double));
     steps = malloc(sizeof(hyg_sgpe_step) * (nst + 1));
-    if (!mo.rows || !mo.lgk || !mo.h || !mo.g || !mo.Hm1s || !mo.gm1s || !mo.exs || !theta || !am || !av ||
-        !gprev || !gcur || !phiP || !phiC || !steps) {
+    if (!mo.rows || !mo.lgk || !mo.h || !mo.g || !mo.Hm1s || !mo.gm1s || !mo.exs || !mo.gk ||
+        (mo.pc.kest && !mo.dgk) || !theta || !am || !av || !gprev || !gcur || !phiP || !phiC || !steps) {
       rc = HYG_ENOMEM;
       goto pe_fail;
     }
     hyg_sgpe_steps_fill(pe, nst + 1, steps);
     hyg_sgpe_lgk_fill(mo.pc.kappa, K, mo.rcap, mo.lgk);
+    if (mo.pc.kest) hyg_sgpe_dgk_fill(mo.pc.kappa, K, mo.rcap, mo.dgk);
     memcpy(theta, p->theta, sizeof(double) * dim);
     sgm_pe_rebuild(&mo, theta, 1 + every + 1);
     if (theta_out) memcpy(theta_out, theta, sizeof(double) * dim);
@@ -491,12 +504,18 @@ static int sg_chain_core(const hyg_sg_params* p, const hyg_sg_pe_params* pe, con
       if (mo.pe) {
         /* updatePhi (OnlineParameterEstimation.h:118-150): phiCurr from phiPrev
          * (gradients of the log transition density, singleGroup.h:641-717) */
-        const int jw = K * (K - 1);
+        const int jw = K * (K - 1), jk = K * K; /* omega / kappa blocks of theta */
         for (int n = 0; n < M; ++n) {
           const int a = anc[n];
           const hyg_sgpe_row* w = sgm_pe_row(&mo, dP[a], rP[a]);
-          for (int j = 0; j < dim; ++j)
-            phiC[(size_t)n * dim + j] = phiP[(size_t)a * dim + j] + ((j == jw + rC[n]) ? w->gcont : 0.0);
+          /* the kappa index of a continuation (:688-692): -grad(idxKappa) rho / (1 - rho)
+           * with grad(idxKappa) = 0 never written, i.e. -0.0 where that branch runs
+           * (!exit && rho < 1, i.e. a finite log(1 - rho)), else the zeroed vector */
+          const double gkap = (w->cont > -INFINITY) ? -0.0 : 0.0;
+          for (int j = 0; j < dim; ++j) {
+            const double g = (j == jw + rC[n]) ? w->gcont : (j == jk + rC[n]) ? gkap : 0.0;
+            phiC[(size_t)n * dim + j] = phiP[(size_t)a * dim + j] + g;
+          }
         }
         const int nch = hyg_sgpe_fresh_chunks(K), rows = 256 / nch;
         for (int q = 0; q < K; ++q) {
@@ -617,11 +636,12 @@ int oracle_sg_chain_refstruct(const hyg_sg_params* p, const uint16_t* meth, cons
   sg_refcounts rc = {meth, tot, S};
   return sg_chain_core(p, NULL, NULL, T, seed, chain_id, probs, nparts_out, NULL, &rc);
 }
-/* theta_out [1 + (T - 1) / every][K^2] */
+/* theta_out [1 + (T - 1) / every][K^2, or K (K + 1) with kappa estimated] */
 int oracle_sg_chain_pe(const hyg_sg_params* p, const hyg_sg_pe_params* pe, const double* E, int T, uint64_t seed,
                        uint64_t chain_id, double* probs, double* theta_out) {
   return sg_chain_core(p, pe, E, T, seed, chain_id, probs, NULL, theta_out, NULL);
 }
+double oracle_sg_digamma(double x) { return hyg_digamma(x); }
 int oracle_sg_pe_hazard(const hyg_sg_params* p, const double* theta, int L, hyg_sgpe_row* rows, int32_t* Lr) {
   /* hazard rows of the estimation path for tests: rows [K][L] */
   hyg_sg_pe_params pe = {1, 0, 200, 0, 0.1, 0.01};
@@ -638,8 +658,14 @@ int oracle_sg_pe_hazard(const hyg_sg_params* p, const double* theta, int L, hyg_
   mo.h = malloc(sizeof(double) * L); mo.g = malloc(sizeof(double) * L);
   mo.Hm1s = malloc(sizeof(double) * L); mo.gm1s = malloc(sizeof(double) * L);
   mo.exs = malloc(L);
-  if (!mo.rows || !mo.lgk || !mo.h || !mo.g || !mo.Hm1s || !mo.gm1s || !mo.exs) { sgm_free(&mo); return HYG_ENOMEM; }
+  mo.gk = malloc(sizeof(double) * L);
+  mo.dgk = mo.pc.kest ? malloc(sizeof(double) * (size_t)K * L) : NULL;
+  if (!mo.rows || !mo.lgk || !mo.h || !mo.g || !mo.Hm1s || !mo.gm1s || !mo.exs || !mo.gk || (mo.pc.kest && !mo.dgk)) {
+    sgm_free(&mo);
+    return HYG_ENOMEM;
+  }
   hyg_sgpe_lgk_fill(mo.pc.kappa, K, L, mo.lgk);
+  if (mo.pc.kest) hyg_sgpe_dgk_fill(mo.pc.kappa, K, L, mo.dgk);
   sgm_pe_rebuild(&mo, theta, L);
   memcpy(rows, mo.rows, sizeof(hyg_sgpe_row) * (size_t)K * L);
   for (int r = 0; r < K; ++r) Lr[r] = mo.Lr[r];

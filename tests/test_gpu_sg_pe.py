@@ -191,18 +191,38 @@ def test_pe_batched_chains_bit_exact(lib, sg):
         r0 += nr
 
 
-def test_pe_kappa_estimated_is_unsupported(lib, sg):
-    p = sg.make_params(K=6)
-    p.is_kappa_fixed, p.theta_len = 0, 42
-    for i in range(36, 42):
-        p.theta[i] = np.log(2.0)
-    h = _model(lib, p, 100, 100)
+KAPPA_CASES = [
+    # K, T, S, coverage, data seed, N_max, every, use_adam, normalise, kappa, seed
+    (6, 3000, 2, 12.0, 11, 250, 200, 1, 0, (2.0, 1.5, 3.0, 0.7, 2.5, 5.0), 0),  # pipeline settings, kappa estimated
+    (4, 1500, 3, 8.0, 12, 30, 25, 0, 1, (1.2, 2.0, 0.4, 8.0), 1),               # L1-normalised plain steps
+    (3, 600, 2, 10.0, 13, 250, 20, 1, 0, (2.0, 2.0, 2.0), 2),
+]
+
+
+@pytest.mark.parametrize("K,T,S,cov,dseed,Nmax,every,adam,norm,kappa,seed", KAPPA_CASES)
+def test_pe_kappa_estimated_bit_exact(lib, sg, K, T, S, cov, dseed, Nmax, every, adam, norm, kappa, seed):
+    """--is_kappa_fixed FALSE: theta of K (K + 1) entries; the kernel's score
+    drops the kappa coordinates (identically 0, include/hyg_sg_pe.h) where the
+    oracle carries all K (K + 1) as singleGroup.h:641-706 writes them: every
+    regime probability and theta row bit-identical, log kappa unmoved."""
+    meth, tot, mu, sgm = _data(K, T, S, cov, dseed)
+    omega = sg.DEFAULT_OMEGA if K == 6 else [0.93] * K
+    p = sg.make_params(K=K, mu=mu, sigma=sgm, P=_uniform_P(K), omega=omega, Nmax=Nmax, kappa=kappa,
+                       kappa_fixed=False)
+    pe = _pe(adam, norm, every, lr_fac=0.01 if adam else 1e-4)
+    E = sg.emission(p, meth, tot)
+    chain_id = (7 << 32) | seed
+    ref = _oracle(sg, p, pe, E, seed, chain_id)
+    assert ref["status"] == 0 and ref["theta"].shape[1] == K * (K + 1)
+    h = _model(lib, p, max(int(tot.max()), 1), T + 10)
     try:
-        meth = np.zeros((10, 1), np.uint16)
-        tot = np.full((10, 1), 5, np.uint16)
-        out, th = np.zeros((10, 6)), np.zeros((1, 42))
-        rc = lib.hyg_sg_run_chain_host_pe(h, C.byref(_pe(1, 0, 200)), _ptr(meth), _ptr(tot), 1, 10, 0, 0,
-                                          _ptr(out), _ptr(th))
-        assert rc == -5, rc
+        out = np.full((T, K), np.nan)
+        th = np.full(ref["theta"].shape, np.nan)
+        rc = lib.hyg_sg_run_chain_host_pe(h, C.byref(pe), _ptr(np.ascontiguousarray(meth)),
+                                          _ptr(np.ascontiguousarray(tot)), S, T, seed, chain_id, _ptr(out), _ptr(th))
+        assert rc == 0, lib.hyg_last_error()
     finally:
         lib.hyg_sg_model_destroy(h)
+    _assert_same(out, th, ref)
+    np.testing.assert_array_equal(th[:, K * K:], np.tile(np.log(np.asarray(kappa, float)), (th.shape[0], 1)))
+    assert not np.array_equal(th[0, :K * K], th[-1, :K * K])

@@ -98,7 +98,7 @@ def test_estimate_parameters_and_regimes_then_infer(tmp_path):
 
     _, rows = _read_csv(str(out / f"theta_{chrom}.csv.gz"))
     np.testing.assert_array_equal(np.array([float(v[0]) for v in rows]), last)
-    p_hat, om_hat = sgc.model_from_theta(last, 6)
+    p_hat, om_hat, _ = sgc.model_from_theta(last, 6)
     head, rows = _read_csv(str(out / f"p_{chrom}.csv.gz"))
     assert head == [f"regime_{r + 1}" for r in range(6)]
     np.testing.assert_array_equal(np.array(rows, dtype=np.float64), p_hat)
@@ -112,6 +112,70 @@ def test_estimate_parameters_and_regimes_then_infer(tmp_path):
     # correctly rounded for 17-digit text: within 3 ulp of the engine's theta
     th_inf = cli.read_theta(str(out), chrom)
     assert np.all(np.abs(th_inf - last) <= 3 * np.spacing(np.abs(last))), np.max(np.abs(th_inf - last))
+    res = tmp_path / "res"
+    assert cli.main(["infer", "--chrom", chrom, "--data_dir", str(data), "--single_group_dir", str(out),
+                     "--results_dir", str(res), "--seed", "0", "--batch", "0", "--mu", MU, "--sigma", SIGMA]) == 0
+    assert os.path.exists(str(res / f"chrom_{chrom}_0" / "optimal_regime_probs_2400_0.npz"))
+
+
+@pytest.mark.timeout(300)
+def test_estimate_parameters_with_kappa_estimated(tmp_path):
+    """--is_kappa_fixed FALSE (bin/estimate_parameters_and_regimes:104-107):
+    theta of K (K + 1) entries drawn from the prior, the trace and the oracle's
+    rows equal, kappa.csv = exp(final log kappa) (:363-365), and `hygeia
+    infer` reads the 42-entry theta file as the reference does (omega's logits
+    from the last K entries, run_inference_two_groups.py:88)."""
+    from hygeia_amd import cli
+    from hygeia_amd import single_group as sgc
+    from hygeia_amd import synthetic as syn
+    from oracle import sg_binding as sg
+
+    chrom, T, S, every, seed = "9", 1201, 2, 50, 5
+    d = syn.simulate(T, S, S, K=6, seed=73, coverage=25.0)
+    data = tmp_path / "data"
+    data.mkdir()
+    pos = syn.positions(T)
+    _write(str(data / f"positions_{chrom}.txt.gz"), pos)
+    for g in ("control", "case"):
+        _write(str(data / f"n_total_reads_{g}_{chrom}.txt.gz"), d[f"tot_{g}"])
+        _write(str(data / f"n_methylated_reads_{g}_{chrom}.txt.gz"), d[f"meth_{g}"])
+    out = tmp_path / "sg"
+    argv = ["estimate_parameters_and_regimes", "--mu", MU, "--sigma", SIGMA, "--u", "3",
+            "--n_methylated_reads_csv_file", str(data / f"n_methylated_reads_control_{chrom}.txt.gz"),
+            "--genomic_positions_csv_file", str(data / f"positions_{chrom}.txt.gz"),
+            "--n_total_reads_csv_file", str(data / f"n_total_reads_control_{chrom}.txt.gz"),
+            "--regime_probabilities_csv_file", str(out / f"regimes_{chrom}.csv.gz"),
+            "--theta_trace_csv_file", str(out / f"theta_trace_{chrom}.csv.gz"),
+            "--p_csv_file", str(out / f"p_{chrom}.csv.gz"), "--kappa_csv_file", str(out / f"kappa_{chrom}.csv.gz"),
+            "--omega_csv_file", str(out / f"omega_{chrom}.csv.gz"), "--theta_file", str(out / f"theta_{chrom}.csv.gz"),
+            "--estimate_regime_probabilities", "--estimate_parameters", "--randomise_rng_seed", "FALSE",
+            "--rng_seed", str(seed), "--n_steps_without_parameter_update", str(every), "--is_kappa_fixed", "FALSE"]
+    assert cli.main(argv) == 0
+
+    meth, tot = d["meth_control"][1:], d["tot_control"][1:]
+    theta0 = np.random.default_rng(seed).standard_normal(42)
+    p = sg.make_params(K=6, mu=[float(x) for x in MU.split(",")], sigma=[float(x) for x in SIGMA.split(",")], u=3,
+                       kappa=np.exp(theta0[36:]), kappa_fixed=False)
+    for i, v in enumerate(theta0):
+        p.theta[i] = v
+    ref = sg.chain_pe(p, sg.make_pe(every=every), sg.emission(p, meth, tot), seed, 0)
+    assert ref["status"] == 0 and ref["theta"].shape[1] == 42
+    n = T - 1
+    _, rows = _read_csv(str(out / f"regimes_{chrom}.csv.gz"))
+    cols = list(zip(*rows))
+    for r in range(6):
+        assert list(cols[1 + r]) == list(sgc.r_format_column(ref["regime_probs"][:, r])), r
+    head, rows = _read_csv(str(out / f"theta_trace_{chrom}.csv.gz"))
+    assert head == [f"theta_{j + 1}" for j in range(42)] and len(rows) == n
+    np.testing.assert_array_equal(np.array(rows, dtype=np.float64), ref["theta"][np.arange(n) // every])
+    last = ref["theta"][(n - 1) // every]
+    np.testing.assert_array_equal(last[36:], theta0[36:])  # log kappa never moves
+    _, rows = _read_csv(str(out / f"kappa_{chrom}.csv.gz"))
+    np.testing.assert_array_equal(np.array([float(v[0]) for v in rows]), np.exp(last[36:]))
+    _, rows = _read_csv(str(out / f"theta_{chrom}.csv.gz"))
+    assert len(rows) == 42
+    th_inf = cli.read_theta(str(out), chrom)
+    np.testing.assert_array_equal(cli.control_theta(th_inf, 6), np.concatenate([th_inf[:30], th_inf[36:]]))
     res = tmp_path / "res"
     assert cli.main(["infer", "--chrom", chrom, "--data_dir", str(data), "--single_group_dir", str(out),
                      "--results_dir", str(res), "--seed", "0", "--batch", "0", "--mu", MU, "--sigma", SIGMA]) == 0

@@ -208,5 +208,106 @@ def test_determinism_golden_and_unsupported(sg):
     # theta moved, P rows stay on the simplex, omega in (0, 1)
     assert not np.array_equal(a["theta"][0], a["theta"][-1])
     p.is_kappa_fixed = 0
-    p.theta_len = 42
-    assert sg.chain_pe(p, pe, E[:10], 0, 0)["status"] == -5  # HYG_EUNSUPPORTED
+    p.theta_len = 40  # kappa estimated needs K (K + 1) = 42 entries
+    assert sg.chain_pe(p, pe, E[:10], 0, 0)["status"] == -1  # HYG_EINVAL
+
+
+def test_digamma_vs_scipy(sg):
+    from scipy import special
+
+    for x in [1e-3, 0.01, 0.1, 0.5, 1.0, 1.4616321449683623, 2.0, 3.7, 9.99, 10.0, 10.5, 50.0, 1e3, 65537.25]:
+        assert sg.digamma(x) == pytest.approx(float(special.digamma(x)), rel=1e-14, abs=1e-14), x
+    assert math.isnan(sg.digamma(0.0)) and math.isnan(sg.digamma(-1.0))
+
+
+def _ref_rows_kappa(K, u, kappa, omega, L):
+    """extendAuxiliaryQuantities (singleGroup.h:271-335) with isKappaFixed_
+    false, restated literally for one regime, and the omega coordinate of the
+    gradient it then feeds (:657-668: the kappa derivative, written into the
+    omega index): rows (log rho, log(1 - rho), gomg, gcont) up to the exit
+    onset, with scipy's gammaln / digamma in place of libm / R's."""
+    from scipy import special
+
+    w, k = omega, kappa
+    gl = 2.0 + math.exp(-w) + math.exp(w)  # gradLogitEvaluatedAtInverseLogit (misc.h:92-95)
+    bigH, gOB, gKB = {}, {}, {}
+    ex_prev = False
+    out = []
+    for d in range(L):
+        if d < u - 1:
+            bigH[d] = gOB[d] = gKB[d] = 0.0
+            out.append((-np.inf, 0.0, 0.0, 0.0))
+            continue
+        x = d + 1 - u
+        lh = math.exp(special.gammaln(x + k) - special.gammaln(k) - special.gammaln(x + 1.0)
+                      + k * math.log(1.0 - w) + x * math.log(w))
+        Hm1 = bigH.get(d - 1, 0.0)
+        if ex_prev or Hm1 >= 1.0:
+            bigH[d - 1] = Hm1 = 0.99999
+            rho, exd = 1.0, True
+        else:
+            bigH[d] = Hm1 + lh
+            rho, exd = lh / (1.0 - Hm1), False
+        gO = (x / w - k / (1.0 - w)) * gl
+        gOB[d] = gOB.get(d - 1, 0.0) + lh * gO
+        gK = k * (special.digamma(x + k) - special.digamma(k) - math.log(1.0 - w))
+        gKB[d] = gOB.get(d - 1, 0.0) + lh * gK  # the omega bigH gradient (:329)
+        gomg = gK + gKB.get(d - 1, 0.0) / (1.0 - Hm1)
+        base = 0.0 if exd else math.log(rho)
+        cont = math.log(1.0 - rho) if (not exd and rho <= 1.0) else -np.inf
+        gcont = (-gomg * rho) / (1.0 - rho) if (not exd and rho < 1.0) else 0.0
+        out.append((base, cont, gomg, gcont))
+        if exd:
+            break
+        ex_prev = exd
+    return np.array(out)
+
+
+@pytest.mark.parametrize("omega,kappa", [(0.8, 2.0), (0.95, 0.6), (0.99, 4.5)])
+def test_kappa_estimated_hazard_rows_literal(sg, omega, kappa):
+    K, u, L = 2, 3, 300
+    p = sg.make_params(K=K, omega=(omega, omega), u=u, kappa=(kappa, kappa), kappa_fixed=False)
+    rows, Lr = sg.pe_hazard(p, np.array(p.theta[:K * (K + 1)]), L)
+    ref = _ref_rows_kappa(K, u, kappa, omega, L)
+    # compare while the survival prod(1 - rho) stays above 1e-6 (the sequential
+    # bigH sums lose digits where 1 - bigH is tiny)
+    n = min(Lr[0], ref.shape[0])
+    rho = np.where(np.arange(n) >= u - 1, np.exp(ref[:n, 0]), 0.0)
+    alive = np.cumprod(1.0 - rho)
+    m = max(int(np.argmax(alive < 1e-6)) if np.any(alive < 1e-6) else n, u + 5)
+    np.testing.assert_allclose(rows[0, u - 1:m, 0], ref[u - 1:m, 0], rtol=1e-10)
+    np.testing.assert_allclose(rows[0, u - 1:m, 2], ref[u - 1:m, 2], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(rows[0, u - 1:m, 3], ref[u - 1:m, 3], rtol=1e-9, atol=1e-12)
+    # the kappa derivative differs from the omega one the fixed path carries
+    pf = sg.make_params(K=K, omega=(omega, omega), u=u, kappa=kappa)
+    rf, _ = sg.pe_hazard(pf, np.array(pf.theta[:K * K]), L)
+    np.testing.assert_array_equal(rf[0, :m, 0], rows[0, :m, 0])
+    assert not np.allclose(rf[0, u - 1:m, 2], rows[0, u - 1:m, 2])
+
+
+def test_kappa_estimated_chain(sg):
+    """Estimated kappa: log kappa never moves (its score is identically 0, the
+    reference's gradient never writing the kappa index, singleGroup.h:664-692);
+    with learning rate 0 the chain is the fixed-kappa chain at kappa =
+    exp(log kappa); with ADAM theta's P / omega entries move along a different
+    path from the fixed-kappa run (the omega coordinate follows d log rho /
+    d theta_kappa)."""
+    K, T, u = 3, 400, 3
+    kappa = (1.5, 2.0, 3.0)
+    meth, tot, mu, sgm = _data(K, T, seed=4)
+    pk = sg.make_params(K=K, mu=mu, sigma=sgm, P=_P_uniform(K), omega=[0.9] * K, u=u, kappa=kappa, kappa_fixed=False)
+    kap = np.exp(np.log(np.asarray(kappa)))
+    pf = sg.make_params(K=K, mu=mu, sigma=sgm, P=_P_uniform(K), omega=[0.9] * K, u=u, kappa=kap)
+    E = sg.emission(pk, meth, tot)
+    pe = sg.make_pe(every=20)
+    a = sg.chain_pe(pk, pe, E, 3, 1)
+    assert a["status"] == 0 and a["theta"].shape == (1 + (T - 1) // 20, K * (K + 1))
+    np.testing.assert_array_equal(a["theta"][:, K * K:], np.tile(np.log(np.asarray(kappa)), (a["theta"].shape[0], 1)))
+    b = sg.chain_pe(pf, pe, E, 3, 1)
+    assert b["status"] == 0
+    np.testing.assert_array_equal(a["theta"][:, :K * (K - 1)][0], b["theta"][:, :K * (K - 1)][0])
+    assert not np.array_equal(a["theta"][-1, :K * K], b["theta"][-1])
+    z = sg.make_pe(every=20, lr_factor=0.0)
+    a0, b0 = sg.chain_pe(pk, z, E, 3, 1), sg.chain_pe(pf, z, E, 3, 1)
+    np.testing.assert_array_equal(a0["regime_probs"], b0["regime_probs"])
+    np.testing.assert_array_equal(a0["theta"][:, :K * K], b0["theta"])

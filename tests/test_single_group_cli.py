@@ -57,7 +57,7 @@ def test_theta_round_trip_transposes_p():
     # block r = log of column r without its diagonal entry
     for r in range(K):
         np.testing.assert_allclose(theta[r * (K - 1):(r + 1) * (K - 1)], np.log(np.delete(p[:, r], r)))
-    q, om = sgc.model_from_theta(theta, K)
+    q, om, _ = sgc.model_from_theta(theta, K)
     pt = p.T / p.T.sum(1, keepdims=True)
     np.testing.assert_allclose(q, pt, rtol=1e-12)
     np.testing.assert_allclose(om, omega, rtol=1e-12)
