@@ -142,7 +142,7 @@ struct SgShared {
 
 struct SgLay {
   size_t st, lw, w, base, cont;  // [2][NT]: current / previous particle sets, alternating per step
-  size_t anc, lwres, logq, sidx, cum, xk, xi, BK, logP, red, lsev, scr, meanb, okb, logm, logQ, psil, sh, total;
+  size_t anc, lwres, logq, sidx, cum, xk, xi, BK, logP, red, scr, meanb, okb, logm, logQ, psil, sh, total;
   size_t pm, gfr, gct, pei, rpu;  // parameter estimation: model, per-particle gradient entries [2][NT], ints,
                                   // regime if d >= u else -1 [2][NT] (int8)
   int nl;  // psi slots resident in LDS (slot ids 0 .. nl-1; the rest live in the workspace)
@@ -183,7 +183,6 @@ __host__ __device__ inline SgLay sg_layout(int K, int cap, bool pe) {
   l.BK = o; o = sg_align(o + 8 * (size_t)K * NT);
   l.logP = o; o = sg_align(o + 8 * (size_t)K * K);
   l.red = o; o = sg_align(o + sg_red_bytes(K, NW));
-  l.lsev = o; o = sg_align(o + 8 * 2 * (size_t)K);
   l.scr = o; o = sg_align(o + 8 * (size_t)NW * NT);
   l.meanb = o; o = sg_align(o + 8 * (size_t)kSgChunk * K);
   l.okb = o; o = sg_align(o + (size_t)kSgChunk * K);
@@ -481,29 +480,31 @@ __device__ __forceinline__ void sg_bitonic(uint64_t& key, int& idx, uint64_t* xk
   }
 }
 
-// The same network on one 64-bit word per thread: the log-weight key's top 56
-// bits with 255 - idx in the low byte, so ties of the word order by ascending
-// idx and a compare-exchange is one 64-bit compare and two selects (the pair
-// sort above: three compares, their merge and three selects). Descending words
-// are the pair order except inside a run of keys that agree on the top 56 bits
-// and differ below them; the caller checks the order it uses (sg_chain_kernel).
+// The order of sg_bitonic on one 64-bit word per thread (the log-weight key's
+// top 56 bits with 255 - idx in the low byte, so ties of the word order by
+// ascending idx; descending words are the pair order except inside a run of
+// keys that agree on the top 56 bits and differ below them: the caller checks
+// the order it uses, sg_chain_kernel), by ranks: each key wave sorts its 64
+// words descending (the network's stages k <= 64, every wave in the final
+// direction), the four runs meet in LDS, and each word's position is its
+// rank, the sum over the runs of
+// the words above it (its lane in its own run; a 7-probe binary search in
+// the others, the four searches interleaved). The words are distinct (255 -
+// idx in the low byte), so the ranks are a permutation and the result is the
+// network's. Two barriers and 21 in-wave stages in place of the three
+// cross-wave stages and 33 in-wave stages of the full network (round 6: the
+// sort 4.4 k -> 3.6 k cycles per chr1 step, profiles/r06r_phases_sg_c2.log).
 template <int NB>
-__device__ __forceinline__ void sg_bitonic_packed(uint64_t& key, uint64_t* xk) {
-  constexpr int NT = kSgThreads;
+__device__ __forceinline__ void sg_rank_sort_packed(uint64_t& key, uint64_t* xk) {
+  constexpr int NT = kSgThreads, NR = NT / 64;
   const int tid = threadIdx.x;
   const bool real = (NB == NT) || tid < NT;
-  int buf = 0;
 #pragma unroll
-  for (int k = 2; k <= NT; k <<= 1) {
+  for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      uint64_t pk = key;
-      if (j >= 64) {
-        if (real) xk[buf * NB + tid] = key;
-        lds_barrier();
-        if (real) pk = xk[buf * NB + (tid ^ j)];
-        buf ^= 1;
-      } else if (real) {
+      if (real) {
+        uint64_t pk;
         switch (j) {
           case 1: pk = xshfl64<1>(key); break;
           case 2: pk = xshfl64<2>(key); break;
@@ -512,21 +513,31 @@ __device__ __forceinline__ void sg_bitonic_packed(uint64_t& key, uint64_t* xk) {
           case 16: pk = xshfl64<16>(key); break;
           default: pk = xshfl64<32>(key); break;
         }
-      }
-      if (j < 64) {
-        if (real) {
-          const uint64_t lower = lanes_bit_clear(j);
-          const uint64_t same = (k < 64) ? ~(lower ^ lanes_bit_clear(k < 64 ? k : 1))
-                                         : (((wave_id() * 64) & k) == 0 ? lower : ~lower);
-          const uint64_t take = ~(same ^ wave_ballot(pk > key));
-          key = lane_select64(take, key, pk);
-        }
-      } else if (real) {
-        const bool up = (tid & k) == 0, lower = (tid & j) == 0;
-        if ((lower == up) ? (pk > key) : !(pk > key)) key = pk;
+        const uint64_t lower = lanes_bit_clear(j);
+        const uint64_t same = (k < 64) ? ~(lower ^ lanes_bit_clear(k < 64 ? k : 1)) : lower;
+        const uint64_t take = ~(same ^ wave_ballot(pk > key));
+        key = lane_select64(take, key, pk);
       }
     }
   }
+  if (real) xk[tid] = key;
+  lds_barrier();
+  if (real) {
+    int pos[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) pos[r] = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) pos[r] += (xk[64 * r + pos[r] + step - 1] > key) ? step : 0;
+    }
+    int rank = 0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) rank += pos[r] + ((xk[64 * r + pos[r]] > key) ? 1 : 0);
+    xk[NB + rank] = key;
+  }
+  lds_barrier();
+  if (real) key = xk[NB + tid];
 }
 __device__ __forceinline__ uint64_t sg_pack_key(uint64_t okey, int idx, uint64_t keep) {
   return (okey & keep) | (uint64_t)(255 - idx);
@@ -605,7 +616,6 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
   unsigned long long* Elimb = (unsigned long long*)(Amax + K);  // [K][2] 51-bit limbs of E_r ([K][3] reserved)
   double* Gq = (double*)(Elimb + 3 * K);          // [K][K] G[r][q]
   double* mqv = Gq + K * K;                       // [K] m_q
-  double* lsev = (double*)(smem + lay.lsev);
   double* logm = (double*)(smem + lay.logm);
   double* logQ = (double*)(smem + lay.logQ);
   SgShared& sh = *(SgShared*)(smem + lay.sh);
@@ -749,7 +759,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         // packed words: exact wherever the order is used (the optimal branch
         // re-checks it against w below, the keep-top path with the full keys)
         uint64_t lkey = sg_pack_key((tid < Np) ? sg_okey(plw) : 0, tid & (NT - 1), md.key_keep);
-        sg_bitonic_packed<NB>(lkey, xk);
+        sg_rank_sort_packed<NB>(lkey, xk);
         const int lidx = sg_packed_idx(lkey);
         if (!PE) { SG_PH(12); }
         const double* wP = w_ + pb * NT;
@@ -1096,7 +1106,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       {
         // the continuing particles' part of the block max and finite count of
         // the new log-weights rides on this barrier; the fresh particles' part
-        // is added from lsev below (no reduction of its own)
+        // is added from lsv below (no reduction of its own)
         const double cm = wave_max(nlw);  // -inf beyond the continuing particles
         const int cn = __builtin_popcountll(wave_ballot(tid < M && hyg_isfinite(nlw)));
         if (lane == 0) {
@@ -1148,10 +1158,13 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       if (!PE) { SG_PH(17); }
       lds_barrier();
       if (!PE) { SG_PH(11); }
-      if (wv == 0) {
-        // wave 0: lane r converts regime r's exact sum E_r once, lane q forms
-        // S_q = sum_r G[r][q] E_r with the E_r read across lanes (readlane, no
-        // LDS round trip per term), in r order as before (the same FMA chain)
+      // every wave: lane r converts regime r's exact sum E_r, lane q forms
+      // S_q = sum_r G[r][q] E_r with the E_r read across lanes (readlane), in r
+      // order (the same FMA chain), and row q's log-normaliser lsq and 1 / S_q;
+      // the values are read across lanes below (the same bits in every wave:
+      // no LDS hand-off, no barrier)
+      double lsq, isq;
+      {
         double Er = 0.0;
         if (lane < K) {
           const unsigned long long* el = Elimb + 2 * lane;
@@ -1170,26 +1183,30 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
         double S = 0.0;
 #pragma unroll
         for (int r = 0; r < K; ++r) S = HYG_FMA(g[r], d_of(rdlane64(u_of(Er), r)), S);
-        if (lane < K) {
-          lsev[lane] = (m > HYG_NINF) ? m + hyg_log(S) : HYG_NINF;  // log-normaliser of row q
-          lsev[K + lane] = (m > HYG_NINF) ? 1.0 / S : 0.0;
-        }
+        lsq = (m > HYG_NINF) ? m + hyg_log(S) : HYG_NINF;
+        isq = (m > HYG_NINF) ? 1.0 / S : 0.0;
       }
+      auto lsev_of = [&](int q) { return d_of(rdlane64(u_of(lsq), q)); };  // q wave-uniform
       if (!PE) { SG_PH(18); }
-      lds_barrier();
       if (!PE) { SG_PH(19); }
 #pragma unroll
       for (int j = 0; j < KH; ++j) {  // this thread's entries of the backward kernels (record of step t)
         const int q = q0 + j < K ? q0 + j : K - 1;
-        BKr[j] = (q0 + j < K && lsev[q] > HYG_NINF) ? (ea * Gq[vr * K + q]) * lsev[K + q] : 0.0;
+        const double lq = lsev_of(q), iq = d_of(rdlane64(u_of(isq), q));
+        BKr[j] = (q0 + j < K && lq > HYG_NINF) ? (ea * Gq[vr * K + q]) * iq : 0.0;
         if (PE && pn < Np && q0 + j < K) BK[q * NT + pn] = BKr[j];
       }
+      double lsv[K];  // row q's log-normaliser in every lane (the fresh particles, the normalisation)
+#pragma unroll
+      for (int q = 0; q < K; ++q) lsv[q] = lsev_of(q);
       if (tid >= M && tid < N) {
         const int q = tid - M;
-        double e = et[0];
+        double e = et[0], lb = lsv[0];
 #pragma unroll
-        for (int qq = 1; qq < K; ++qq) e = (q == qq) ? et[qq] : e;
-        const double lb = lsev[q];
+        for (int qq = 1; qq < K; ++qq) {
+          e = (q == qq) ? et[qq] : e;
+          lb = (q == qq) ? lsv[qq] : lb;
+        }
         nlw = (lb > HYG_NINF) ? lb + e : HYG_NINF;
         nst = sg_pack(1, q);
       }
@@ -1200,7 +1217,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       sg_drain_stores();
       if (!PE) { SG_PH(20); }
       // block max and finite count of the N new log-weights: the continuing
-      // particles' wave partials and the K fresh ones (lsev[q] + log g_t(q), as
+      // particles' wave partials and the K fresh ones (lsv[q] + log g_t(q), as
       // formed above), the same values as one block reduction (a max is exact)
       double mx = redc[0];
       fin = redn[0];
@@ -1211,7 +1228,7 @@ sg_chain_kernel(SgModelDev md, const SgChainDev* __restrict__ chains, int n_chai
       }
 #pragma unroll
       for (int q = 0; q < K; ++q) {
-        const double lb = lsev[q];
+        const double lb = lsv[q];
         const double f = (lb > HYG_NINF) ? lb + et[q] : HYG_NINF;
         mx = dmax(mx, f);
         fin += hyg_isfinite(f) ? 1 : 0;
