@@ -1024,6 +1024,58 @@ struct Bitonic {
     else if constexpr (KK < 64 * (NT / 64) * R) Bitonic<NT, R, 2 * KK, KK>::run(e, buf, ib);
   }
 };
+// The order of Bitonic<64 NSW, 1, 2, 1> (ascending) of distinct keys, one per
+// lane of the first NSW waves, by ranks: each wave sorts its 64 keys ascending
+// (the network's stages KK <= 64, every wave in the final direction), the
+// runs meet in buf[0, 64 NSW), and each key's position is its rank, the sum
+// over the runs of the keys below it (its lane in its own run; a 7-probe
+// binary search in the others, interleaved); buf[64 NSW, 128 NSW) receives the
+// sorted keys. Two barriers and 21 in-wave stages in place
+// of the network's three cross-wave stages and 33 in-wave stages. The other
+// waves of the workgroup pass the same barriers and run `idle` between them.
+template <int J, int KK>
+__device__ __forceinline__ void rank_sort_stage(uint64_t& e) {
+  constexpr uint64_t pat = keep_min_pattern<1, J, KK>();  // KK = 64: every wave as wave 0 (ascending)
+  const uint64_t o = xshfl64<J>(e);
+  const uint64_t lt = wave_ballot(o < e);
+  e = lane_select64(~(pat ^ lt), e, o);
+}
+template <int J, int KK>
+struct RankRuns {
+  __device__ static __forceinline__ void run(uint64_t& e) {
+    rank_sort_stage<J, KK>(e);
+    if constexpr (J > 1) RankRuns<J / 2, KK>::run(e);
+    else if constexpr (KK < 64) RankRuns<KK, 2 * KK>::run(e);
+  }
+};
+template <int NSW, class Idle>
+__device__ __forceinline__ uint64_t rank_sort_asc(uint64_t e, uint64_t* buf, bool sorter, Idle idle) {
+  const int base = (int)(threadIdx.x >> 6) * 64 + lane_id();
+  if (sorter) {
+    RankRuns<1, 2>::run(e);
+    buf[base] = e;
+  }
+  lds_barrier();
+  if (!sorter) {
+    idle();
+  } else {
+    int pos[NSW];
+#pragma unroll
+    for (int r = 0; r < NSW; ++r) pos[r] = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+#pragma unroll
+      for (int r = 0; r < NSW; ++r) pos[r] += (buf[64 * r + pos[r] + step - 1] < e) ? step : 0;
+    }
+    int rank = 0;
+#pragma unroll
+    for (int r = 0; r < NSW; ++r) rank += pos[r] + ((buf[64 * r + pos[r]] < e) ? 1 : 0);
+    buf[64 * NSW + rank] = e;
+  }
+  lds_barrier();
+  return sorter ? buf[64 * NSW + base] : e;
+}
+
 // workgroup barriers of a bitonic sort of n keys held R per lane (one per
 // cross-wave stage): the waves of a larger workgroup that take no part in the
 // sort pass the same number of barriers
@@ -1276,11 +1328,11 @@ __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB,
   uint64_t e[1];
   hyg_u192 f = hyg_u192_zero(), inc = hyg_u192_zero();
   if (sorter) {
-    e[0] = (base < nA) ? srt[base] : ~0ull;
-    int ib = 0;
-    Bitonic<64 * NSW, 1, 2, 1>::run(e, (uint64_t*)scr, ib);
+    // (distinct pads above every key past nA: the rank sort needs distinct keys)
+    e[0] = (base < nA) ? srt[base] : ~0ull - (uint64_t)base;
+    e[0] = rank_sort_asc<NSW>(e[0], (uint64_t*)scr, true, []() {});
     TPH(27);
-    // (every wave loaded its keys before the first cross-wave barrier)
+    // (every wave loaded its keys before the sort's first barrier)
     srt[base] = e[0];
     const float m = hyg_expf(key_value(e[0]));
     f = hyg_fix149f((base < nA) ? m : 0.0f);
@@ -1289,19 +1341,18 @@ __device__ __forceinline__ int top_set_finish1(uint64_t* srt, int nA, bool hasB,
     if (lane == 63) wtot[wave_id()] = inc;
   } else {
     // SPLIT: the waves that do not sort sum the outside masses meanwhile,
-    // wave NSW + v the lists v and v + NNS (NW <= 2 NNS): the first before the
-    // sort's first cross-wave barrier, the second after its last (both before
-    // the first barrier delay the sort: measured)
+    // wave NSW + v the lists v and v + NNS (NW <= 2 NNS): the first while the
+    // sorting waves sort their runs, the second while they search the ranks
+    // (between the sort's two barriers)
     static_assert(!SPLIT || NW <= 2 * NNS, "two lists per idle wave");
-    constexpr int nb = bitonic_lds_stages(64 * NSW, 1);
     hyg_u128 n128 = hyg_u128_zero();
     hyg_u192 m192 = hyg_u192_zero();
     const int v = wave_id() - NSW;
     if (SPLIT && hasB) list_mass(lb, v, n128, m192);  // uniform
-#pragma unroll
-    for (int i = 0; i < nb; ++i) lds_barrier();
+    (void)rank_sort_asc<NSW>(0, (uint64_t*)scr, false, [&]() {
+      if (SPLIT && hasB && v + NNS < NW) list_mass(lb, v + NNS, n128, m192);
+    });
     if (SPLIT && hasB) {
-      if (v + NNS < NW) list_mass(lb, v + NNS, n128, m192);
       if (lb.narrow) { m192.w0 = n128.lo; m192.w1 = n128.hi; m192.w2 = 0; }
       const hyg_u192 ws = wave_sum192(m192);
       if (lane == 0) lb.part_tot[v] = ws;
