@@ -196,6 +196,7 @@ KAPPA_CASES = [
     (6, 3000, 2, 12.0, 11, 250, 200, 1, 0, (2.0, 1.5, 3.0, 0.7, 2.5, 5.0), 0),  # pipeline settings, kappa estimated
     (4, 1500, 3, 8.0, 12, 30, 25, 0, 1, (1.2, 2.0, 0.4, 8.0), 1),               # L1-normalised plain steps
     (3, 600, 2, 10.0, 13, 250, 20, 1, 0, (2.0, 2.0, 2.0), 2),
+    (12, 400, 2, 20.0, 14, 250, 30, 1, 0, (0.8, 1.0, 1.5, 2.0, 2.5, 3.0, 4.0, 0.5, 1.2, 2.2, 6.0, 1.7), 3),  # 256 threads
 ]
 
 
